@@ -1,0 +1,281 @@
+/*
+ * primeuncore.h — C ABI of the MI355X-native PriME uncore timing engine.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ *   UncoreManager::uncore_access  (reference src/uncore_manager.cpp:82-85)
+ *     -> System::access           (reference src/system.cpp:144-168)
+ * i.e. set-associative tag/LRU lookups (Cache), directory / shared-LLC MESI
+ * transitions, XY mesh Network/Link timing with the Graphite history-tree +
+ * M/G/1 queue model, and fixed-latency Dram.
+ *
+ * Plain C: pointers, sizes and PODs only; no exceptions cross this boundary.
+ * Every entry point returns 0 (or a non-negative value) on success and a
+ * negative PU_E* code on failure; pu_last_error() gives the message.
+ *
+ * The engine keeps R independent "replicas" of the uncore on one GPU (one
+ * wavefront each).  Replica r is a complete System instance; requests for
+ * replica r are processed strictly in the order given (the canonical order),
+ * exactly as the reference's single-threaded msgHandler loop would
+ * (reference src/prime.cpp:120-137).
+ */
+#ifndef PRIMEUNCORE_H
+#define PRIMEUNCORE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PU_MAX_LEVELS 4
+
+/* error codes */
+#define PU_OK          0
+#define PU_EINVAL    (-22)
+#define PU_ENOMEM    (-12)
+#define PU_ENODEV    (-19)
+#define PU_ERANGE    (-34)
+#define PU_EIO        (-5)
+#define PU_ENOTSUP   (-95)
+#define PU_ESTATE    (-71)   /* engine hit a state the reference treats as UB */
+
+/* memory request types — reference src/common.h:61-66 (MemType) */
+#define PU_RD 0
+#define PU_WR 1
+#define PU_WB 2
+
+/* ------------------------------------------------------------------------
+ * Configuration: plain-C mirror of the reference's XmlSim/XmlSys/XmlCache/
+ * XmlNetwork structs (reference src/xml_parser.h:43-100), same field
+ * meaning.  `cache[]` is inline (at most PU_MAX_LEVELS levels).
+ * ---------------------------------------------------------------------- */
+typedef struct pu_cache_cfg {          /* XmlCache, xml_parser.h:47-55 */
+    int32_t  level;
+    int32_t  share;
+    int32_t  access_time;
+    int32_t  _pad;
+    uint64_t size;
+    uint64_t block_size;
+    uint64_t num_ways;
+} pu_cache_cfg;
+
+typedef struct pu_net_cfg {            /* XmlNetwork, xml_parser.h:57-65 */
+    int32_t  data_width;
+    int32_t  header_flits;
+    int32_t  net_type;                 /* 0 = 2D mesh, 1 = 3D mesh */
+    int32_t  _pad;
+    uint64_t router_delay;
+    uint64_t link_delay;
+    uint64_t inject_delay;
+} pu_net_cfg;
+
+typedef struct pu_sys_cfg {            /* XmlSys, xml_parser.h:69-89 */
+    int32_t  sys_type;                 /* 0 directory, 1 bus */
+    int32_t  protocol_type;            /* 0 full map, 1 limited pointer */
+    int32_t  max_num_sharers;
+    int32_t  page_size;
+    int32_t  tlb_enable;
+    int32_t  shared_llc;
+    int32_t  verbose_report;
+    int32_t  dram_access_time;
+    double   cpi_nonmem;
+    int32_t  num_levels;
+    int32_t  num_cores;
+    double   freq;
+    int32_t  bus_latency;
+    int32_t  page_miss_delay;
+    pu_net_cfg   network;
+    pu_cache_cfg directory_cache;
+    pu_cache_cfg tlb_cache;
+    pu_cache_cfg cache[PU_MAX_LEVELS];
+} pu_sys_cfg;
+
+typedef struct pu_sim_cfg {            /* XmlSim, xml_parser.h:92-100 */
+    int32_t  max_msg_size;
+    int32_t  num_recv_threads;
+    int32_t  thread_sync_interval;
+    int32_t  proc_sync_interval;
+    int32_t  syscall_cost;
+    int32_t  _pad;
+    pu_sys_cfg sys;
+} pu_sim_cfg;
+
+/* Parse a config_prime XML file (schema of reference tools/config_prime:62-198;
+ * replaces XmlParser::parse, reference src/xml_parser.cpp:684-718, including its
+ * required-field counts 5/13/4/6/6/6*L and the optional max_num_sharers,
+ * net_type and inject_delay).  Returns 0 or PU_EINVAL. */
+int pu_config_load_xml(const char* path, pu_sim_cfg* out);
+int pu_config_parse_xml(const char* text, size_t len, pu_sim_cfg* out);
+/* Write the config back out in config_prime's XML layout. */
+int pu_config_write_xml(const pu_sim_cfg* cfg, char* buf, size_t cap, size_t* written);
+
+/* ------------------------------------------------------------------------
+ * Requests.  One pu_req per MsgMem record (reference src/common.h:49-59),
+ * already resolved to a core id (ThreadSched, reference src/thread_sched.cpp:55)
+ * and tagged with the Pin process rank (prime.cpp:125 prog_id = MPI source).
+ * batch_start = 1 marks the first request of a MEM_REQUESTS message: the
+ * running-delay rule of prime.cpp:129 restarts there:
+ *     D = 0 at batch start;  d_i = access(core, req_i, timer_i + D);  D += d_i - 1
+ * ---------------------------------------------------------------------- */
+typedef struct pu_req {
+    uint64_t addr;         /* MsgMem.addr_dmem */
+    int64_t  timer;        /* MsgMem.timer (core cycle when issued) */
+    int32_t  core;         /* core id */
+    int32_t  prog_id;      /* program (Pin process rank, >= 1) */
+    uint8_t  mem_type;     /* PU_RD / PU_WR */
+    uint8_t  batch_start;  /* 1 = first request of a message */
+    uint16_t _pad0;
+    int32_t  _pad1;
+} pu_req;                  /* 32 bytes */
+
+/* ------------------------------------------------------------------------
+ * Statistics — every number System::report prints (reference
+ * src/system.cpp:956-1111, network.cpp:310-323, dram.cpp:50-55) plus the
+ * extra counters the parity harness obtains from the reference with
+ * -Wl,--wrap.
+ * ---------------------------------------------------------------------- */
+typedef struct pu_level_stats {
+    uint64_t ins;
+    uint64_t miss;
+    uint64_t evict;
+    uint64_t wb;
+} pu_level_stats;
+
+typedef struct pu_stats {
+    uint64_t net_accesses;          /* Network::num_access */
+    uint64_t net_distance;          /* Network::total_distance (= link visits) */
+    uint64_t net_total_delay;
+    uint64_t net_router_delay;
+    uint64_t net_link_delay;
+    uint64_t net_inject_delay;
+    uint64_t dram_accesses;
+    uint64_t total_bus_contention;
+    int64_t  total_num_broadcast;
+    int32_t  num_levels;
+    int32_t  _pad;
+    pu_level_stats level[PU_MAX_LEVELS];   /* data caches, aggregated per level */
+    pu_level_stats directory;              /* directory / shared-LLC slices */
+    pu_level_stats tlb;
+    /* extra counters */
+    uint64_t link_flits;            /* sum of packet_len over Link::access */
+    uint64_t mg1_calls;             /* QueueModelMG1::computeQueueDelay calls */
+    uint64_t lockdown_calls;        /* Cache::lockDown calls (share/inval visits) */
+    uint64_t bus_accesses;          /* Bus::access calls */
+    uint64_t requests;              /* uncore_access calls */
+    uint64_t error_flags;           /* PU_ERRF_* bits; 0 for a valid run */
+} pu_stats;
+
+#define PU_ERRF_CORE_RANGE   (1ull << 0)  /* core_id >= num_cores (system.cpp:147) */
+#define PU_ERRF_WB_MISS      (1ull << 1)  /* WB missed at home: NULL deref in ref (Q13) */
+#define PU_ERRF_EMPTY_SHARER (1ull << 2)  /* *sharer_set.begin() on empty set */
+#define PU_ERRF_QUEUE        (1ull << 3)  /* queue-model precondition violated */
+#define PU_ERRF_NEG_DELAY    (1ull << 4)  /* batch delay went negative (prime.cpp:130) */
+
+/* ------------------------------------------------------------------------
+ * Engine lifetime and the hot path.
+ * ---------------------------------------------------------------------- */
+typedef struct pu_handle pu_handle;
+
+/* Replaces UncoreManager::init (reference src/uncore_manager.cpp:46-50 ->
+ * System::init system.cpp:47-141, ThreadSched::init thread_sched.cpp:44).
+ * Allocates `num_replicas` independent uncores on HIP device `device`.
+ * Returns NULL on failure (see pu_last_error). */
+pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device);
+void       pu_destroy(pu_handle* h);
+/* Return all replicas to the just-initialised state (no reallocation). */
+int        pu_reset(pu_handle* h);
+int        pu_num_replicas(const pu_handle* h);
+/* Device bytes held by one replica's state. */
+uint64_t   pu_replica_bytes(const pu_handle* h);
+
+/* Thread -> core map (reference src/thread_sched.cpp:55-91; identical quirks:
+ * first free core, a core is marked busy with prog_id, dealloc frees only
+ * when core_stat == 1).  Shared by all replicas. */
+int pu_alloc_core(pu_handle* h, int prog_id, int thread_id);
+int pu_dealloc_core(pu_handle* h, int prog_id, int thread_id);
+int pu_get_core_id(pu_handle* h, int prog_id, int thread_id);
+
+/* Single-request compatibility path: UncoreManager::uncore_access
+ * (uncore_manager.cpp:82-85).  Operates on replica 0; `*addr` is updated in
+ * place like InsMem::addr_dmem (system.cpp:916).  Returns the delay (>= 0)
+ * or -1 for core_id >= num_cores, like System::access (system.cpp:147-150). */
+int pu_access(pu_handle* h, int core_id, int prog_id, int mem_type,
+              uint64_t* addr, int64_t timer);
+
+/* Batch path from host memory: the per-message loop of prime.cpp:120-137 for
+ * replica `replica`.  delay_out[i] receives uncore_access's return value for
+ * reqs[i] (may be NULL).  Synchronous.  Returns 0 or PU_E*. */
+int pu_access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n,
+                    int32_t* delay_out);
+
+/* Batch path from device memory, all replicas at once, asynchronous on
+ * `hip_stream` (a hipStream_t; NULL = the default stream).  Replica r
+ * processes d_reqs[d_off[r] .. d_off[r+1]) and writes d_delay over the same
+ * range.  d_off holds num_replicas+1 entries and lives in device memory.
+ * Nothing is copied to or from the host. */
+int pu_run_device(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off,
+                  int32_t* d_delay, void* hip_stream);
+int pu_synchronize(pu_handle* h);
+
+/* Per-core completion cycle of the last request each core issued
+ * (last timer_i + D + d_i); out has num_cores entries (-1 = no request). */
+int pu_core_completion(pu_handle* h, int replica, int64_t* out, size_t n);
+
+/* Statistics and the report text of UncoreManager::report
+ * (uncore_manager.cpp:87-98 -> ThreadSched::report, System::report) for one
+ * replica.  With include_time == 0 the wall-clock line is omitted so the
+ * text can be compared byte-for-byte.  Returns the full length (like
+ * snprintf); writes at most cap bytes including the terminating NUL. */
+int pu_stats_get(pu_handle* h, int replica, pu_stats* out);
+long pu_report(pu_handle* h, int replica, int include_time, char* buf, size_t cap);
+
+/* Device-time of the last pu_run_device / pu_access_batch launch, in ms,
+ * measured with HIP events on the engine's stream. */
+double pu_last_kernel_ms(pu_handle* h);
+
+const char* pu_last_error(void);
+const char* pu_version(void);
+
+/* ------------------------------------------------------------------------
+ * Synthetic request streams.  Deterministic: one splitmix64
+ * per core seeded seed*2^32 + core; per core timer += 1 + U{0..3}; a core
+ * stops at each quantum barrier (q+1)*quantum (core_manager.cpp:104-198);
+ * messages of <= max_msg requests never span a barrier; canonical order is
+ * quantum-major, then core id, batch-atomic.
+ * ---------------------------------------------------------------------- */
+#define PU_STREAM_PRIVATE_STREAMING 1  /* C1: blackscholes-like */
+#define PU_STREAM_SHARED_UNIFORM    2  /* C2: canneal-like */
+#define PU_STREAM_MULTIPROGRAM      3  /* C3: SPEC-like mix, 4 programs */
+#define PU_STREAM_UNIFORM_HOTSPOT   4  /* C4: uniform 2^20 lines + 64-line hotspot */
+#define PU_STREAM_PRODUCER_CONSUMER 5  /* C5: core pairs sharing buffers */
+#define PU_STREAM_UNIFORM           6  /* C4(i): pure uniform */
+
+typedef struct pu_stream_params {
+    int32_t  kind;             /* PU_STREAM_* */
+    int32_t  num_cores;
+    uint64_t seed;
+    int32_t  quantum;          /* thread_sync_interval, e.g. 1000 */
+    int32_t  num_quanta;       /* quanta to generate */
+    int32_t  max_msg;          /* max_msg_size, e.g. 100 */
+    int32_t  num_progs;        /* programs; core c belongs to prog 1 + c*num_progs/num_cores */
+    int64_t  max_requests;     /* stop after this many requests (<=0: no cap) */
+    int32_t  write_pct;        /* percent writes; <0 = kind default */
+    int32_t  _pad;
+} pu_stream_params;
+
+/* Number of requests the stream holds (call first to size the buffer). */
+int64_t pu_stream_count(const pu_stream_params* p);
+/* Fill out[0..cap) in canonical order; returns the number written or PU_E*. */
+int64_t pu_stream_generate(const pu_stream_params* p, pu_req* out, size_t cap);
+/* The (prog_id, thread_id) of core c in a generated stream. */
+int pu_stream_thread_of(const pu_stream_params* p, int core, int* prog_id, int* thread_id);
+
+/* Trace files ("PUTRACE1": header, thread table, pu_req records). */
+int pu_trace_write(const char* path, const pu_req* reqs, size_t n,
+                   const int32_t* thread_prog, const int32_t* thread_id, int num_threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PRIMEUNCORE_H */

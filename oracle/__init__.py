@@ -1,0 +1,199 @@
+"""TEST INFRASTRUCTURE ONLY — the parity oracle.
+
+* `CpuRef`: the CPU restatement of the reference uncore (oracle/cpu_ref.cpp,
+  built into oracle/libpu_oracle.so).  Checker for the HIP engine and the
+  "port" CPU baseline.
+* `RefUncore`: the reference's own uncore compiled in place from
+  /root/reference/src (oracle/_ref/libprime_ref.so; only where it was built).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this package.  The product (primesim_amd) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import tempfile
+from typing import Optional
+
+import numpy as np
+
+from primesim_amd import _abi as A
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_LIB = os.path.join(HERE, "libpu_oracle.so")
+REF_LIB = os.path.join(HERE, "_ref", "libprime_ref.so")
+
+_olib: Optional[C.CDLL] = None
+_rlib: Optional[C.CDLL] = None
+
+
+def oracle_lib() -> C.CDLL:
+    global _olib
+    if _olib is None:
+        if not os.path.exists(ORACLE_LIB):
+            raise RuntimeError(f"{ORACLE_LIB} missing: run `make -C oracle`")
+        L = C.CDLL(ORACLE_LIB)
+        P = C.POINTER
+        L.cpuref_create.restype = C.c_void_p
+        L.cpuref_create.argtypes = [P(A.SimCfg), C.c_char_p, C.c_size_t]
+        L.cpuref_destroy.argtypes = [C.c_void_p]
+        L.cpuref_alloc_core.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.cpuref_run.restype = C.c_long
+        L.cpuref_run.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.cpuref_stats.argtypes = [C.c_void_p, P(A.Stats)]
+        L.cpuref_completion.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.cpuref_cache_counters.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]
+        L.cpuref_queue_run.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                       P(C.c_uint64)]
+        _olib = L
+    return _olib
+
+
+def ref_available() -> bool:
+    return os.path.exists(REF_LIB)
+
+
+def ref_lib() -> C.CDLL:
+    global _rlib
+    if _rlib is None:
+        if not ref_available():
+            raise RuntimeError(f"{REF_LIB} missing: run `make -C oracle ref` where /root/reference exists")
+        L = C.CDLL(REF_LIB)
+        P = C.POINTER
+        L.ref_create.restype = C.c_void_p
+        L.ref_create.argtypes = [C.c_char_p, P(C.c_int)]
+        L.ref_get_config.argtypes = [C.c_void_p, P(A.SimCfg)]
+        L.ref_alloc_core.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.ref_get_core_id.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.ref_run.restype = C.c_long
+        L.ref_run.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.ref_completion.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.ref_report.restype = C.c_long
+        L.ref_report.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t]
+        L.ref_counters.argtypes = [C.c_void_p]
+        L.ref_destroy.argtypes = [C.c_void_p]
+        L.ref_queue_run.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.ref_network_run.restype = C.c_long
+        L.ref_network_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64,
+                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                      C.c_char_p, C.c_char_p, C.c_size_t]
+        _rlib = L
+    return _rlib
+
+
+class CpuRef:
+    """CPU restatement of System + the prime.cpp request loop."""
+
+    def __init__(self, cfg: A.SimCfg):
+        err = C.create_string_buffer(256)
+        self._h = oracle_lib().cpuref_create(C.byref(cfg), err, 256)
+        if not self._h:
+            raise RuntimeError(f"cpuref_create: {err.value.decode()}")
+        self.num_cores = cfg.sys.num_cores
+        self.num_levels = cfg.sys.num_levels
+
+    def close(self):
+        if self._h:
+            oracle_lib().cpuref_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def alloc_core(self, prog: int, thread: int) -> int:
+        return oracle_lib().cpuref_alloc_core(self._h, prog, thread)
+
+    def run(self, reqs: np.ndarray) -> tuple[np.ndarray, int]:
+        reqs = np.ascontiguousarray(reqs, dtype=A.REQ_DTYPE)
+        d = np.zeros(len(reqs), dtype=np.int32)
+        rc = oracle_lib().cpuref_run(self._h, reqs.ctypes.data, len(reqs), d.ctypes.data)
+        return d, int(rc)
+
+    def stats(self) -> A.Stats:
+        s = A.Stats()
+        oracle_lib().cpuref_stats(self._h, C.byref(s))
+        return s
+
+    def completion(self) -> np.ndarray:
+        out = np.zeros(self.num_cores, dtype=np.int64)
+        oracle_lib().cpuref_completion(self._h, out.ctypes.data, self.num_cores)
+        return out
+
+    def cache_counters(self, level: int, ncaches: int) -> np.ndarray:
+        out = np.zeros(ncaches * 4, dtype=np.uint64)
+        oracle_lib().cpuref_cache_counters(self._h, level, out.ctypes.data, out.size)
+        return out.reshape(-1, 4)
+
+
+def cpuref_queue(min_proc: int, t: np.ndarray, p: np.ndarray) -> tuple[np.ndarray, int]:
+    t = np.ascontiguousarray(t, dtype=np.uint64)
+    p = np.ascontiguousarray(p, dtype=np.uint64)
+    out = np.zeros(len(t), dtype=np.uint64)
+    calls = C.c_uint64(0)
+    oracle_lib().cpuref_queue_run(min_proc, t.ctypes.data, p.ctypes.data, len(t), out.ctypes.data, C.byref(calls))
+    return out, int(calls.value)
+
+
+REF_COUNTER_NAMES = ("link_visits", "link_flits", "mg1_calls", "lockdown_calls", "bus_accesses",
+                     "transmits", "dram_accesses")
+
+
+class RefUncore:
+    """The reference's own System (compiled in place) + the prime.cpp loop."""
+
+    def __init__(self, xml_path: str):
+        err = C.c_int(0)
+        self._h = ref_lib().ref_create(xml_path.encode(), C.byref(err))
+        if not self._h:
+            raise RuntimeError(f"reference XmlParser rejected {xml_path}")
+        cfg = A.SimCfg()
+        ref_lib().ref_get_config(self._h, C.byref(cfg))
+        self.cfg = cfg
+        self.num_cores = cfg.sys.num_cores
+
+    def close(self):
+        if self._h:
+            ref_lib().ref_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def alloc_core(self, prog: int, thread: int) -> int:
+        return ref_lib().ref_alloc_core(self._h, prog, thread)
+
+    def run(self, reqs: np.ndarray) -> tuple[np.ndarray, int]:
+        reqs = np.ascontiguousarray(reqs, dtype=A.REQ_DTYPE)
+        d = np.zeros(len(reqs), dtype=np.int32)
+        rc = ref_lib().ref_run(self._h, reqs.ctypes.data, len(reqs), d.ctypes.data)
+        return d, int(rc)
+
+    def completion(self) -> np.ndarray:
+        out = np.zeros(self.num_cores, dtype=np.int64)
+        ref_lib().ref_completion(self._h, out.ctypes.data, self.num_cores)
+        return out
+
+    def report(self) -> str:
+        fd, tmp = tempfile.mkstemp(suffix=".report")
+        os.close(fd)
+        n = ref_lib().ref_report(self._h, tmp.encode(), None, 0)
+        fd, tmp = tempfile.mkstemp(suffix=".report")
+        os.close(fd)
+        buf = C.create_string_buffer(n + 1)
+        ref_lib().ref_report(self._h, tmp.encode(), buf, n + 1)
+        return buf.value.decode()
+
+    @staticmethod
+    def counters() -> dict:
+        out = (C.c_uint64 * 7)()
+        ref_lib().ref_counters(out)
+        return dict(zip(REF_COUNTER_NAMES, [int(x) for x in out]))
+
+
+def ref_queue(min_proc: int, t: np.ndarray, p: np.ndarray) -> np.ndarray:
+    t = np.ascontiguousarray(t, dtype=np.uint64)
+    p = np.ascontiguousarray(p, dtype=np.uint64)
+    out = np.zeros(len(t), dtype=np.uint64)
+    ref_lib().ref_queue_run(min_proc, t.ctypes.data, p.ctypes.data, len(t), out.ctypes.data)
+    return out

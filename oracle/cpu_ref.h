@@ -1,0 +1,36 @@
+/* cpu_ref.h — TEST INFRASTRUCTURE ONLY.  C API of the CPU restatement of the
+ * reference uncore (oracle/cpu_ref.cpp).  Imported only by tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the checker /
+ * baseline — never by the product path. */
+#ifndef PU_CPU_REF_H
+#define PU_CPU_REF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../include/primeuncore.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+void* cpuref_create(const pu_sim_cfg* cfg, char* err, size_t errcap);
+void cpuref_destroy(void* h);
+int cpuref_alloc_core(void* h, int prog, int thread);
+/* prime.cpp:120-137 loop over reqs; delays may be NULL.  Returns 0 or the
+ * index+1 of the first request whose running batch delay went negative. */
+long cpuref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays);
+int cpuref_stats(void* h, pu_stats* out);
+int cpuref_completion(void* h, int64_t* out, size_t n);
+/* Per-cache counters: level l (0..num_levels-1) or l == num_levels for the
+ * directory slices; out holds ncaches*4 entries (ins, miss, evict, wb). */
+int cpuref_cache_counters(void* h, int level, uint64_t* out, size_t n);
+
+/* Graphite history-tree queue model alone: min_proc, (t_i, p_i) -> delay_i. */
+int cpuref_queue_run(uint64_t min_proc, const uint64_t* t, const uint64_t* p, size_t n,
+                     uint64_t* delay_out, uint64_t* mg1_calls);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,116 @@
+"""ctypes mirror of include/primeuncore.h (structs, constants).
+
+Shared by the product binding (primesim_amd.uncore) and the test harness.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+PU_MAX_LEVELS = 4
+
+PU_RD, PU_WR, PU_WB = 0, 1, 2
+
+PU_STREAM_PRIVATE_STREAMING = 1
+PU_STREAM_SHARED_UNIFORM = 2
+PU_STREAM_MULTIPROGRAM = 3
+PU_STREAM_UNIFORM_HOTSPOT = 4
+PU_STREAM_PRODUCER_CONSUMER = 5
+PU_STREAM_UNIFORM = 6
+
+PU_ERRF_CORE_RANGE = 1 << 0
+PU_ERRF_WB_MISS = 1 << 1
+PU_ERRF_EMPTY_SHARER = 1 << 2
+PU_ERRF_QUEUE = 1 << 3
+PU_ERRF_NEG_DELAY = 1 << 4
+
+
+class CacheCfg(C.Structure):
+    _fields_ = [
+        ("level", C.c_int32), ("share", C.c_int32), ("access_time", C.c_int32), ("_pad", C.c_int32),
+        ("size", C.c_uint64), ("block_size", C.c_uint64), ("num_ways", C.c_uint64),
+    ]
+
+
+class NetCfg(C.Structure):
+    _fields_ = [
+        ("data_width", C.c_int32), ("header_flits", C.c_int32), ("net_type", C.c_int32), ("_pad", C.c_int32),
+        ("router_delay", C.c_uint64), ("link_delay", C.c_uint64), ("inject_delay", C.c_uint64),
+    ]
+
+
+class SysCfg(C.Structure):
+    _fields_ = [
+        ("sys_type", C.c_int32), ("protocol_type", C.c_int32), ("max_num_sharers", C.c_int32),
+        ("page_size", C.c_int32), ("tlb_enable", C.c_int32), ("shared_llc", C.c_int32),
+        ("verbose_report", C.c_int32), ("dram_access_time", C.c_int32), ("cpi_nonmem", C.c_double),
+        ("num_levels", C.c_int32), ("num_cores", C.c_int32), ("freq", C.c_double),
+        ("bus_latency", C.c_int32), ("page_miss_delay", C.c_int32),
+        ("network", NetCfg), ("directory_cache", CacheCfg), ("tlb_cache", CacheCfg),
+        ("cache", CacheCfg * PU_MAX_LEVELS),
+    ]
+
+
+class SimCfg(C.Structure):
+    _fields_ = [
+        ("max_msg_size", C.c_int32), ("num_recv_threads", C.c_int32), ("thread_sync_interval", C.c_int32),
+        ("proc_sync_interval", C.c_int32), ("syscall_cost", C.c_int32), ("_pad", C.c_int32),
+        ("sys", SysCfg),
+    ]
+
+
+class LevelStats(C.Structure):
+    _fields_ = [("ins", C.c_uint64), ("miss", C.c_uint64), ("evict", C.c_uint64), ("wb", C.c_uint64)]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("net_accesses", C.c_uint64), ("net_distance", C.c_uint64), ("net_total_delay", C.c_uint64),
+        ("net_router_delay", C.c_uint64), ("net_link_delay", C.c_uint64), ("net_inject_delay", C.c_uint64),
+        ("dram_accesses", C.c_uint64), ("total_bus_contention", C.c_uint64), ("total_num_broadcast", C.c_int64),
+        ("num_levels", C.c_int32), ("_pad", C.c_int32),
+        ("level", LevelStats * PU_MAX_LEVELS), ("directory", LevelStats), ("tlb", LevelStats),
+        ("link_flits", C.c_uint64), ("mg1_calls", C.c_uint64), ("lockdown_calls", C.c_uint64),
+        ("bus_accesses", C.c_uint64), ("requests", C.c_uint64), ("error_flags", C.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        d = {}
+        for name, _ in self._fields_:
+            if name.startswith("_"):
+                continue
+            v = getattr(self, name)
+            if name == "level":
+                for i in range(self.num_levels):
+                    for f in ("ins", "miss", "evict", "wb"):
+                        d[f"L{i}_{f}"] = getattr(v[i], f)
+            elif isinstance(v, LevelStats):
+                for f in ("ins", "miss", "evict", "wb"):
+                    d[f"{name}_{f}"] = getattr(v, f)
+            else:
+                d[name] = v
+        return d
+
+
+class StreamParams(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32), ("num_cores", C.c_int32), ("seed", C.c_uint64), ("quantum", C.c_int32),
+        ("num_quanta", C.c_int32), ("max_msg", C.c_int32), ("num_progs", C.c_int32),
+        ("max_requests", C.c_int64), ("write_pct", C.c_int32), ("_pad", C.c_int32),
+    ]
+
+
+# pu_req as a numpy structured dtype (32 bytes, matches the C struct layout)
+REQ_DTYPE = np.dtype([
+    ("addr", "<u8"), ("timer", "<i8"), ("core", "<i4"), ("prog_id", "<i4"),
+    ("mem_type", "u1"), ("batch_start", "u1"), ("_pad0", "<u2"), ("_pad1", "<i4"),
+])
+assert REQ_DTYPE.itemsize == 32
+assert C.sizeof(SimCfg) == 24 + C.sizeof(SysCfg)
+
+
+def ptr(a: np.ndarray, ctype=C.c_void_p):
+    """Raw pointer to a contiguous numpy array."""
+    assert a.flags["C_CONTIGUOUS"]
+    return C.cast(a.ctypes.data, ctype)

@@ -1,0 +1,867 @@
+// engine.hip — MI355X (gfx950) uncore timing engine: the hot path of
+//   UncoreManager::uncore_access -> System::access   (reference uncore_manager.cpp:82,
+//   system.cpp:144) for sys_type = DIRECTORY (mesi_directory, system.cpp:372-482).
+//
+// Execution model.  The reference is a strictly sequential fold over requests:
+// every request's timing depends on the link-queue, directory and cache state
+// left by all earlier requests, so one uncore instance is
+// executed by ONE wavefront, in canonical order, bit-exactly.  The 64 lanes
+// parallelise the inner loops of each step instead of the requests:
+//   * set probes       lane w holds way w: tag/prog/state match by ballot,
+//                      first-invalid-way by ballot, LRU by a wave argmin
+//                      (lowest way wins ties, cache.cpp:167-179);
+//   * sharer sets      lane k holds bitmap word k; ascending iteration by
+//                      ballot + ctz (std::set<int> order, system.cpp:607);
+//   * link queues      the Graphite history tree is a sorted ring of <=100
+//                      free intervals, lane s%64 holding slots s and s+64;
+//                      the tree search becomes one predicate + ballot, and
+//                      insert/remove become one register shift (shuffles);
+//   * routes           XY(Z) routes are computed arithmetically, so the next
+//                      hop's link record is loaded while this hop is timed.
+// Throughput comes from running many independent replicas (one wavefront
+// each) side by side on the 256 CUs; a replica's state is laid out SoA in
+// HBM as described in geometry.h.
+//
+// All floating point (the M/G/1 fallback, queue_model_m_g_1.cpp:26-35) is
+// IEEE double in the reference's operation order; this file is compiled with
+// -ffp-contract=off so no FMA contraction changes a rounding.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/primeuncore.h"
+#include "geometry.h"
+
+namespace {
+
+constexpr uint32_t ST_I = 0, ST_S = 1, ST_E = 2, ST_M = 3, ST_V = 4, ST_B = 5;
+
+__device__ __forceinline__ int lane_id() { return (int)threadIdx.x; }
+
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+    uint32_t lo = rl32((uint32_t)v, l);
+    uint32_t hi = rl32((uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ uint32_t uni32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    uint32_t lo = uni32((uint32_t)v), hi = uni32((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+    uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ void atomic_add_u64(uint64_t* p, uint64_t v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct Req {
+    uint64_t addr;
+    int32_t prog;
+    int32_t type;
+};
+
+// A set of one cache, as held by the wave: uniform set coordinates plus the
+// lane's own way (lanes >= nways hold an invalid, never-LRU way).
+struct SetView {
+    uint64_t line0;   // global line index of way 0
+    uint64_t set;
+    uint64_t tag;     // tag of the probed address
+    uint64_t mtag;    // per lane
+    int32_t mid;
+    uint32_t mst;
+    int64_t mts;
+};
+
+// One queue (link or bus) as held by the wave: uniform header + two ring
+// slots per lane (physical slots lane and lane+64).
+struct QueueView {
+    uint32_t hw;       // per lane: header dword `lane` (lanes 0..9)
+    uint64_t lf, ls, hf, hs;
+};
+
+template <int NL>
+struct Engine {
+    const Geo* __restrict__ g;
+    char* base;
+    int ln;
+
+    // reference System scratch for the requesting core (delay[core], hit_flag[core])
+    int dly;
+    bool hit;
+
+    // stats accumulated in registers, flushed once per launch
+    uint64_t s_net_acc, s_net_dist, s_net_total, s_net_router, s_net_link, s_net_inject;
+    uint64_t s_dram, s_bus_cont, s_flits, s_mg1, s_lockdown, s_busacc, s_reqs, s_err;
+    int64_t s_bcast;
+
+    template <class T>
+    __device__ __forceinline__ T* at(uint64_t off) const {
+        return reinterpret_cast<T*>(base + off);
+    }
+
+    // ------------------------------------------------------------ queues
+    __device__ __forceinline__ void q_issue(QueueView& v, int q) const {
+        const uint32_t* H = reinterpret_cast<const uint32_t*>(at<QueueHdr>(g->off_qhdr) + q);
+        const QueueSlot* R = at<QueueSlot>(g->off_qring) + (size_t)q * PU_QRING;
+        v.hw = ln < 10 ? H[ln] : 0u;
+        QueueSlot a = R[ln];
+        QueueSlot b = R[ln + 64];
+        v.lf = a.first; v.ls = a.second;
+        v.hf = b.first; v.hs = b.second;
+    }
+
+    // M/G/1 (queue_model_m_g_1.cpp:16-42), reference operation order.
+    __device__ __forceinline__ uint64_t mg1_wait(uint64_t n, double sum, double sum_sq,
+                                                 uint64_t newest) const {
+        if (n == 0) return 0;
+        double nd = (double)n;
+        double mean = sum / nd;
+        double var = (sum_sq / nd) - mean * mean;
+        double mu = 1.0 / (sum / nd);
+        double lambda = nd / (double)newest;
+        if (lambda >= mu) lambda = 0.999 * mu;
+        double inv = 1.0 / (mu * mu);
+        double num = 0.5 * mu;
+        num = num * lambda;
+        num = num * (inv + var);
+        double w = num / (mu - lambda);
+        return (uint64_t)ceil(w);
+    }
+
+    // QueueModelHistoryTree::computeQueueDelay (queue_model_history_tree.cpp:42-125)
+    // on the ring view; writes the queue back.  Returns the queue delay.
+    __device__ uint64_t q_apply(QueueView& v, int q, uint64_t t, uint64_t p, uint64_t minp) {
+        uint32_t head = rl32(v.hw, 0), cnt = rl32(v.hw, 1);
+        uint64_t n = ((uint64_t)rl32(v.hw, 3) << 32) | rl32(v.hw, 2);
+        double sum = __longlong_as_double((long long)(((uint64_t)rl32(v.hw, 5) << 32) | rl32(v.hw, 4)));
+        double sum_sq = __longlong_as_double((long long)(((uint64_t)rl32(v.hw, 7) << 32) | rl32(v.hw, 6)));
+        uint64_t newest = ((uint64_t)rl32(v.hw, 9) << 32) | rl32(v.hw, 8);
+
+        if (cnt >= PU_QMAX) {           // prune the minimum (history_tree.cpp:49-55)
+            head = (head + 1) & (PU_QRING - 1);
+            cnt--;
+        }
+        const uint64_t tp = t + p;
+        uint64_t front_first = head < 64 ? rl64(v.lf, (int)head) : rl64(v.hf, (int)(head - 64));
+        uint64_t d;
+        // pending ring edits
+        int op = 0;  // 0 none, 1 second<-t, 2 first<-x, 3 remove, 4 split
+        uint32_t k = 0;
+        uint64_t nf = 0, node_second = 0;
+        if (front_first > tp) {        // analytical model (history_tree.cpp:58-63)
+            d = mg1_wait(n, sum, sum_sq, newest);
+            s_mg1++;
+        } else {
+            const uint32_t jl = ((uint32_t)ln - head) & (PU_QRING - 1);
+            const uint32_t jh = ((uint32_t)ln + 64 - head) & (PU_QRING - 1);
+            bool pl = jl < cnt && ((v.lf <= t && tp <= v.ls) || (t < v.lf && v.ls - v.lf >= p));
+            bool ph = jh < cnt && ((v.hf <= t && tp <= v.hs) || (t < v.hf && v.hs - v.hf >= p));
+            uint64_t ml = ballot(pl), mh = ballot(ph);
+            // leftmost in logical (ring) order starting at `head`
+            uint32_t slot;
+            if (head < 64) {
+                uint64_t ge = ml & (~0ull << head);
+                if (ge) slot = (uint32_t)__builtin_ctzll(ge);
+                else if (mh) slot = 64 + (uint32_t)__builtin_ctzll(mh);
+                else slot = (uint32_t)__builtin_ctzll(ml);
+            } else {
+                uint64_t ge = mh & (~0ull << (head - 64));
+                if (ge) slot = 64 + (uint32_t)__builtin_ctzll(ge);
+                else if (ml) slot = (uint32_t)__builtin_ctzll(ml);
+                else slot = 64 + (uint32_t)__builtin_ctzll(mh);
+            }
+            if ((ml | mh) == 0) {      // tree search returned NULL: assert in the reference
+                s_err |= PU_ERRF_QUEUE;
+                slot = head;
+            }
+            k = (slot - head) & (PU_QRING - 1);
+            uint64_t f = slot < 64 ? rl64(v.lf, (int)slot) : rl64(v.hf, (int)(slot - 64));
+            uint64_t s = slot < 64 ? rl64(v.ls, (int)slot) : rl64(v.hs, (int)(slot - 64));
+            node_second = s;
+            if (t >= f) {
+                d = 0;
+                if (t - f >= minp) {
+                    op = (s - tp >= minp) ? 4 : 1;
+                } else if (s - tp >= minp) {
+                    op = 2;
+                    nf = tp;
+                } else {
+                    op = 3;
+                }
+            } else {
+                d = f - t;
+                if (s - (f + p) >= minp) {
+                    op = 2;
+                    nf = f + p;
+                } else {
+                    op = 3;
+                }
+            }
+        }
+
+        // ---- apply ring edit (logical positions relative to `head`)
+        uint32_t new_head = head, new_cnt = cnt;
+        bool dl = false, dh = false;
+        uint64_t lf = v.lf, ls = v.ls, hf = v.hf, hs = v.hs;
+        if (op != 0) {
+            const uint32_t jl = ((uint32_t)ln - head) & (PU_QRING - 1);
+            const uint32_t jh = ((uint32_t)ln + 64 - head) & (PU_QRING - 1);
+            if (op == 1 || op == 2) {
+                if (jl == k) { if (op == 1) ls = t; else lf = nf; dl = true; }
+                if (jh == k) { if (op == 1) hs = t; else hf = nf; dh = true; }
+            } else if (op == 3) {
+                if (k == 0) {
+                    new_head = (head + 1) & (PU_QRING - 1);
+                } else {
+                    // logical [k+1, cnt) move down by one: slot s takes slot s+1
+                    const int src = (ln + 1) & 63;
+                    uint64_t a_f = shfl64(v.lf, src), a_s = shfl64(v.ls, src);
+                    uint64_t b_f = shfl64(v.hf, src), b_s = shfl64(v.hs, src);
+                    uint64_t sl_f = ln == 63 ? b_f : a_f, sl_s = ln == 63 ? b_s : a_s;
+                    uint64_t sh_f = ln == 63 ? a_f : b_f, sh_s = ln == 63 ? a_s : b_s;
+                    if (jl >= k && jl + 1 < cnt) { lf = sl_f; ls = sl_s; dl = true; }
+                    if (jh >= k && jh + 1 < cnt) { hf = sh_f; hs = sh_s; dh = true; }
+                }
+                new_cnt = cnt - 1;
+            } else {  // split: node k keeps [first, t], [t+p, second] inserted at k+1
+                const int src = (ln + 63) & 63;
+                uint64_t a_f = shfl64(v.lf, src), a_s = shfl64(v.ls, src);
+                uint64_t b_f = shfl64(v.hf, src), b_s = shfl64(v.hs, src);
+                uint64_t pl_f = ln == 0 ? b_f : a_f, pl_s = ln == 0 ? b_s : a_s;
+                uint64_t ph_f = ln == 0 ? a_f : b_f, ph_s = ln == 0 ? a_s : b_s;
+                if (jl == k) { ls = t; dl = true; }
+                else if (jl == k + 1) { lf = tp; ls = node_second; dl = true; }
+                else if (jl >= k + 2 && jl <= cnt) { lf = pl_f; ls = pl_s; dl = true; }
+                if (jh == k) { hs = t; dh = true; }
+                else if (jh == k + 1) { hf = tp; hs = node_second; dh = true; }
+                else if (jh >= k + 2 && jh <= cnt) { hf = ph_f; hs = ph_s; dh = true; }
+                new_cnt = cnt + 1;
+            }
+        }
+        // ---- M/G/1 update (queue_model_m_g_1.cpp:45-55) — always
+        sum_sq = sum_sq + (double)p * (double)p;
+        sum = sum + (double)p;
+        n = n + 1;
+        uint64_t fin = t + d + p;
+        newest = fin > newest ? fin : newest;
+
+        // ---- write back (owners only)
+        QueueSlot* R = at<QueueSlot>(g->off_qring) + (size_t)q * PU_QRING;
+        if (dl) R[ln] = QueueSlot{lf, ls};
+        if (dh) R[ln + 64] = QueueSlot{hf, hs};
+        if (ln < 10) {
+            uint64_t sb = (uint64_t)__double_as_longlong(sum), qb = (uint64_t)__double_as_longlong(sum_sq);
+            uint32_t w;
+            switch (ln) {
+                case 0: w = new_head; break;
+                case 1: w = new_cnt; break;
+                case 2: w = (uint32_t)n; break;
+                case 3: w = (uint32_t)(n >> 32); break;
+                case 4: w = (uint32_t)sb; break;
+                case 5: w = (uint32_t)(sb >> 32); break;
+                case 6: w = (uint32_t)qb; break;
+                case 7: w = (uint32_t)(qb >> 32); break;
+                case 8: w = (uint32_t)newest; break;
+                default: w = (uint32_t)(newest >> 32); break;
+            }
+            reinterpret_cast<uint32_t*>(at<QueueHdr>(g->off_qhdr) + q)[ln] = w;
+        }
+        return d;
+    }
+
+    // ------------------------------------------------------------ network
+    __device__ __forceinline__ void coords(int id, int& x, int& y, int& z) const {
+        const int w = g->net_width;
+        if (g->net_type == 1) {
+            x = (id % (w * w)) % w;
+            y = (id % (w * w)) / w;
+            z = id / (w * w);
+        } else {
+            x = id % w;
+            y = id / w;
+            z = 0;
+        }
+    }
+    // Network::getLink (network.cpp:213-307): one record per undirected edge.
+    __device__ __forceinline__ int link_of(int x, int y, int z, int dir) const {
+        const int w = g->net_width;
+        int a, b, c;
+        if (g->net_type == 1) {
+            switch (dir) {
+                case 0: a = x; b = y; c = z; break;
+                case 1: a = x - 1; b = y; c = z; break;
+                case 2: a = y - 1; b = z; c = x + w; break;
+                case 3: a = y; b = z; c = x + w; break;
+                case 4: a = z; b = x; c = y + 2 * w; break;
+                default: a = z - 1; b = x; c = y + 2 * w; break;
+            }
+            return (a * w + b) * (3 * w) + c;
+        }
+        switch (dir) {
+            case 0: a = x; b = y; break;
+            case 1: a = x - 1; b = y; break;
+            case 2: a = y - 1; b = x + w; break;
+            default: a = y; b = x + w; break;
+        }
+        return a * (2 * w) + b;
+    }
+    // link of hop h of the X-then-Y-then-Z route from (sx,sy,sz) to (rx,ry,rz)
+    __device__ __forceinline__ int route_link(int h, int sx, int sy, int sz, int rx, int ry, int rz,
+                                              int hx, int hy) const {
+        if (h < hx) {
+            int e = rx > sx;
+            int x = e ? sx + h : sx - h;
+            return link_of(x, sy, sz, e ? 0 : 1);
+        }
+        if (h < hx + hy) {
+            int s = ry > sy;
+            int y = s ? sy + (h - hx) : sy - (h - hx);
+            return link_of(rx, y, sz, s ? 3 : 2);
+        }
+        int u = rz > sz;
+        int z = u ? sz + (h - hx - hy) : sz - (h - hx - hy);
+        return link_of(rx, ry, z, u ? 4 : 5);
+    }
+
+    // Network::transmit (network.cpp:97-160)
+    __device__ uint64_t transmit(int src, int dst, int len, uint64_t timer) {
+        if (src == dst) return 0;
+        const int plen = g->header_flits + (int)ceil((double)len / (double)g->data_width);
+        int sx, sy, sz, rx, ry, rz;
+        coords(src, sx, sy, sz);
+        coords(dst, rx, ry, rz);
+        const int hx = abs(rx - sx), hy = abs(ry - sy), hz = abs(rz - sz);
+        const int hops = hx + hy + hz;
+        const uint64_t router = g->router_delay, link_delay = g->link_delay;
+        uint64_t t = timer + g->inject_delay;
+        QueueView cur, nxt;
+        int qc = route_link(0, sx, sy, sz, rx, ry, rz, hx, hy);
+        q_issue(cur, qc);
+        for (int h = 0; h < hops; h++) {
+            int qn = 0;
+            if (h + 1 < hops) {
+                qn = route_link(h + 1, sx, sy, sz, rx, ry, rz, hx, hy);
+                q_issue(nxt, qn);
+            }
+            t += router;
+            t += q_apply(cur, qc, t, (uint64_t)plen, link_delay) + link_delay;
+            s_flits += (uint64_t)plen;
+            cur = nxt;
+            qc = qn;
+        }
+        t += router;
+        t += (uint64_t)(plen - 1);
+        const uint64_t dist = (uint64_t)hops;
+        s_net_acc++;
+        s_net_total += t - timer;
+        s_net_router += (dist + 1) * router;
+        s_net_link += t - timer - (dist + 1) * router - (uint64_t)(plen - 1) - g->inject_delay;
+        s_net_inject += g->inject_delay;
+        s_net_dist += dist;
+        return t - timer;
+    }
+
+    // ------------------------------------------------------------ sets
+    __device__ __forceinline__ void set_load(SetView& v, const LineMeta* meta, const int64_t* ts,
+                                             uint64_t nsets, uint64_t nways, int offbits, int idxbits,
+                                             uint64_t cache_index, uint64_t addr) const {
+        v.set = (addr >> offbits) % nsets;
+        v.tag = addr >> (offbits + idxbits);
+        v.line0 = (cache_index * nsets + v.set) * nways;
+        if ((uint64_t)ln < nways) {
+            LineMeta m = meta[v.line0 + (uint64_t)ln];
+            v.mtag = m.tag;
+            v.mid = m.id;
+            v.mst = m.state;
+            v.mts = ts[v.line0 + (uint64_t)ln];
+        } else {
+            v.mtag = 0;
+            v.mid = 0;
+            v.mst = ST_I;
+            v.mts = INT64_MAX;
+        }
+    }
+    __device__ __forceinline__ int set_find(const SetView& v, uint64_t nways, int prog) const {
+        uint64_t m = ballot((uint64_t)ln < nways && v.mst != ST_I && v.mid == prog && v.mtag == v.tag);
+        return m ? (int)__builtin_ctzll(m) : -1;
+    }
+    // Cache::replaceLine (cache.cpp:204-235): first invalid way, else LRU
+    // (strictly smaller timestamp, lowest way on ties).  Sets tag/id only.
+    __device__ __forceinline__ int set_replace(SetView& v, LineMeta* meta, uint64_t nways, int offbits,
+                                               int idxbits, int prog, uint32_t* old_state,
+                                               uint64_t* old_addr, int* old_prog) const {
+        uint64_t inv = ballot((uint64_t)ln < nways && v.mst == ST_I);
+        int way;
+        if (inv) {
+            way = (int)__builtin_ctzll(inv);
+            *old_state = ST_I;
+            *old_addr = 0;
+            *old_prog = 0;
+        } else {
+            int64_t bt = v.mts;
+            int bw = (uint64_t)ln < nways ? ln : 64;
+            for (int o = 32; o >= 1; o >>= 1) {
+                int64_t ot = (int64_t)shfl64((uint64_t)bt, ln ^ o);
+                int ow = __shfl(bw, ln ^ o, 64);
+                if (ot < bt || (ot == bt && ow < bw)) {
+                    bt = ot;
+                    bw = ow;
+                }
+            }
+            way = (int)uni32((uint32_t)bw);
+            *old_state = rl32(v.mst, way);
+            *old_addr = (v.set << offbits) | (rl64(v.mtag, way) << (offbits + idxbits));
+            *old_prog = (int)rl32((uint32_t)v.mid, way);
+        }
+        if (ln == way) {
+            v.mtag = v.tag;
+            v.mid = prog;
+            meta[v.line0 + (uint64_t)way] = LineMeta{v.tag, prog, v.mst};
+        }
+        return way;
+    }
+    __device__ __forceinline__ void set_state(SetView& v, LineMeta* meta, int way, uint32_t st) const {
+        if (ln == way) {
+            v.mst = st;
+            meta[v.line0 + (uint64_t)way].state = st;
+        }
+    }
+    __device__ __forceinline__ void set_ts(SetView& v, int64_t* ts, int way, int64_t t) const {
+        if (ln == way) {
+            v.mts = t;
+            ts[v.line0 + (uint64_t)way] = t;
+        }
+    }
+
+    // ------------------------------------------------------------ per-cache bookkeeping
+    __device__ __forceinline__ void mark_alive(int l, int cid) const {
+        // System::init_caches (system.cpp:172-207) creates the cache and its
+        // ancestors on first touch; only the existence bit is observable.
+        for (int k = l; k < NL; k++) {
+            if (ln == (cid & 63)) at<uint32_t>(g->lv[k].off_alive)[cid] = 1u;
+            if (k + 1 < NL) cid = cid * g->lv[k].share / g->lv[k + 1].share;
+        }
+    }
+    __device__ __forceinline__ void count(uint64_t off_cnt, int cid, int which) const {
+        if (ln == 0) atomic_add_u64(at<uint64_t>(off_cnt) + (size_t)cid * 4 + which, 1ull);
+    }
+
+    __device__ __forceinline__ int dram() {
+        s_dram++;
+        return g->dram_access_time;
+    }
+
+    // ------------------------------------------------------------ downward propagation
+    // System::share / System::inval (system.cpp:488-555); LV is the level of `cid`.
+    template <int LV, bool INVAL>
+    __device__ int down(int cid, const Req& r) {
+        const LevelGeo& L = g->lv[LV];
+        uint32_t alive_v = ln == (cid & 63) ? at<uint32_t>(L.off_alive)[cid] : 0u;
+        SetView v;
+        set_load(v, at<LineMeta>(L.off_meta), at<int64_t>(L.off_ts), L.nsets, L.nways, L.offbits, L.idxbits,
+                 (uint64_t)cid, r.addr);
+        if (!rl32(alive_v, cid & 63)) return 0;   // cache never created: NULL in the reference
+        s_lockdown++;
+        int d = L.access_time;
+        int way = set_find(v, L.nways, r.prog);
+        if (way >= 0) {
+            uint32_t st = rl32(v.mst, way);
+            if (INVAL || st == ST_M || st == ST_E) {
+                set_state(v, at<LineMeta>(L.off_meta), way, INVAL ? ST_I : ST_S);
+                d += children<LV, INVAL>(cid, r);
+            }
+        }
+        return d;
+    }
+    // share_children / inval_children (system.cpp:514-572): max over children.
+    template <int LV, bool INVAL>
+    __device__ int children(int cid, const Req& r) {
+        if constexpr (LV == 0) {
+            return 0;
+        } else {
+            const int nc = g->lv[LV].nchildren;
+            int mx = 0;
+            for (int k = 0; k < nc; k++) {
+                int d = down<LV - 1, INVAL>(cid * nc + k, r);
+                mx = d > mx ? d : mx;
+            }
+            return mx;
+        }
+    }
+
+    // ------------------------------------------------------------ sharer bitmaps
+    __device__ __forceinline__ int first_sharer(uint64_t sw, int nw) {
+        uint64_t m = ballot(ln < nw && sw != 0);
+        if (!m) {
+            s_err |= PU_ERRF_EMPTY_SHARER;
+            return 0;
+        }
+        int k = (int)__builtin_ctzll(m);
+        return k * 64 + (int)__builtin_ctzll(rl64(sw, k));
+    }
+    __device__ __forceinline__ int count_sharers(uint64_t sw, int nw) const {
+        int c = ln < nw ? __builtin_popcountll(sw) : 0;
+        for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+        return (int)uni32((uint32_t)c);
+    }
+
+    // home -> sharer -> inval -> home for every sharer in ascending id
+    // (system.cpp:605-618, 660-671, 766-779, 820-831)
+    __device__ int inval_sharers(uint64_t sw, int nw, int home, const Req& r, int64_t base_t) {
+        const int last = NL - 1;
+        int pipe = 0, mx = 0;
+        uint64_t rem = ln < nw ? sw : 0;
+        while (true) {
+            uint64_t m = ballot(rem != 0);
+            if (!m) break;
+            int k = (int)__builtin_ctzll(m);
+            uint64_t word = rl64(rem, k);
+            int p = k * 64 + (int)__builtin_ctzll(word);
+            if (ln == k) rem &= rem - 1;
+            int t = pipe;
+            t += (int)transmit(home, p, 0, (uint64_t)(base_t + t));
+            t += down<last, true>(p, r);
+            t += (int)transmit(p, home, 0, (uint64_t)(base_t + t));
+            mx = t > mx ? t : mx;
+            pipe += g->header_flits;
+        }
+        return mx;
+    }
+    // broadcast to every core (system.cpp:621-633 etc.; N == num_cores enforced)
+    __device__ int broadcast(int home, const Req& r, int64_t base_t) {
+        const int last = NL - 1;
+        int pipe = 0, mx = 0;
+        s_bcast++;
+        for (int i = 0; i < g->num_cores; i++) {
+            int t = pipe;
+            t += (int)transmit(home, i, 0, (uint64_t)(base_t + t));
+            t += down<last, true>(i, r);
+            t += (int)transmit(i, home, 0, (uint64_t)(base_t + t));
+            mx = t > mx ? t : mx;
+            pipe += g->header_flits;
+        }
+        return mx;
+    }
+
+    // ------------------------------------------------------------ home slice
+    // accessSharedCache (system.cpp:734-893) / accessDirectoryCache (577-731)
+    __device__ int access_home(int cid, int home, const Req& r, int64_t timer, uint32_t* out_state) {
+        const DirGeo& D = g->dir;
+        const bool shared = g->shared_llc != 0;
+        const int last = NL - 1;
+        const int blk = (int)g->lv[last].block;
+        const int nw = D.nwords;
+        LineMeta* meta = at<LineMeta>(D.off_meta);
+        int64_t* tsa = at<int64_t>(D.off_ts);
+        uint64_t* sh = at<uint64_t>(D.off_sh);
+        if (ln == (home & 63)) at<uint32_t>(D.off_alive)[home] = 1u;   // home_stat[home] = 1
+        SetView v;
+        set_load(v, meta, tsa, D.nsets, D.nways, D.offbits, D.idxbits, (uint64_t)home, r.addr);
+        int way = set_find(v, D.nways, r.prog);
+        count(D.off_cnt, home, 0);
+        int delay = D.access_time;
+        uint32_t st;
+        if (way < 0 && r.type != PU_WB) {
+            uint32_t old_st;
+            uint64_t old_addr;
+            int old_prog;
+            way = set_replace(v, meta, D.nways, D.offbits, D.idxbits, r.prog, &old_st, &old_addr, &old_prog);
+            uint64_t* lsh = sh + (v.line0 + (uint64_t)way) * (uint64_t)nw;
+            uint64_t sw = ln < nw ? lsh[ln] : 0;
+            if (old_st != ST_I) {
+                count(D.off_cnt, home, 2);
+                Req o{old_addr, old_prog, PU_RD};
+                if (old_st == ST_M || old_st == ST_E) {
+                    int own = first_sharer(sw, nw);
+                    delay += (int)transmit(home, own, 0, (uint64_t)(timer + delay));
+                    delay += down<last, true>(own, o);
+                    int reply = (!shared || old_st == ST_M) ? blk : 0;
+                    delay += (int)transmit(own, home, reply, (uint64_t)(timer + delay));
+                    dram();
+                } else if (old_st == ST_S) {
+                    delay += inval_sharers(sw, nw, home, o, timer + delay);
+                } else if (old_st == ST_B) {
+                    delay += broadcast(home, o, timer + delay);
+                }
+            }
+            st = r.type == PU_WR ? ST_M : ST_E;
+            set_state(v, meta, way, st);
+            count(D.off_cnt, home, 1);
+            if (ln < nw) lsh[ln] = (ln == (cid >> 6)) ? (1ull << (cid & 63)) : 0ull;
+            delay += dram();
+        } else if (way < 0) {
+            s_err |= PU_ERRF_WB_MISS;     // WB missed at home: NULL deref in the reference (Q13)
+            *out_state = ST_I;
+            return delay;
+        } else {
+            st = rl32(v.mst, way);
+            uint64_t* lsh = sh + (v.line0 + (uint64_t)way) * (uint64_t)nw;
+            uint64_t sw = ln < nw ? lsh[ln] : 0;
+            if (r.type == PU_WR) {
+                if (st == ST_M || st == ST_E) {
+                    int own = first_sharer(sw, nw);
+                    delay += (int)transmit(home, own, 0, (uint64_t)(timer + delay));
+                    delay += down<last, true>(own, r);
+                    delay += (int)transmit(own, home, blk, (uint64_t)(timer + delay));
+                } else if (st == ST_S) {
+                    delay += inval_sharers(sw, nw, home, r, timer + delay);
+                    if (!shared) delay += dram();
+                } else if (st == ST_B) {
+                    delay += broadcast(home, r, timer + delay);
+                    if (!shared) delay += dram();
+                }
+                st = ST_M;
+                if (ln < nw) lsh[ln] = (ln == (cid >> 6)) ? (1ull << (cid & 63)) : 0ull;
+            } else if (r.type == PU_RD) {
+                if (st == ST_M || st == ST_E) {
+                    int own = first_sharer(sw, nw);
+                    delay += (int)transmit(home, own, 0, (uint64_t)(timer + delay));
+                    delay += down<last, false>(own, r);
+                    delay += (int)transmit(own, home, blk, (uint64_t)(timer + delay));
+                    st = ST_S;
+                } else if (st == ST_S) {
+                    if (!shared) delay += dram();
+                    if (g->protocol_type == 1 && count_sharers(sw, nw) >= g->max_num_sharers) st = ST_B;
+                } else if (st == ST_B) {
+                    if (!shared) delay += dram();
+                } else if (st == ST_V) {
+                    st = ST_E;
+                }
+                if (ln == (cid >> 6)) lsh[ln] = sw | (1ull << (cid & 63));
+            } else {
+                st = shared ? ST_V : ST_I;
+                if (ln < nw) lsh[ln] = 0ull;
+                dram();
+            }
+            set_state(v, meta, way, st);
+        }
+        *out_state = st == ST_B ? ST_S : st;
+        set_ts(v, tsa, way, timer);
+        return delay;
+    }
+
+    __device__ __forceinline__ int home_of(uint64_t addr) const {
+        // System::allocHomeId (system.cpp:921-936)
+        int hb = (int)((addr >> g->home_offbits) % (uint64_t)(1 << g->home_mask_bits));
+        if (hb < g->N) return hb;
+        return hb % (1 << (g->home_mask_bits - 1));
+    }
+
+    // ------------------------------------------------------------ directory MESI walk
+    // System::mesi_directory (system.cpp:372-482); LV is the level of `cid`.
+    template <int LV>
+    __device__ uint32_t mesi(int cid, const Req& r, int64_t timer) {
+        const LevelGeo& L = g->lv[LV];
+        constexpr bool kLast = LV == NL - 1;
+        LineMeta* meta = at<LineMeta>(L.off_meta);
+        int64_t* tsa = at<int64_t>(L.off_ts);
+        SetView v;
+        set_load(v, meta, tsa, L.nsets, L.nways, L.offbits, L.idxbits, (uint64_t)cid, r.addr);
+        mark_alive(LV, cid);
+        if (L.has_bus) {              // Bus::access (bus.cpp:55-61)
+            QueueView bq;
+            int q = L.bus_q0 + cid;
+            q_issue(bq, q);
+            s_busacc++;
+            uint64_t bl = (uint64_t)g->bus_latency;
+            int db = (int)q_apply(bq, q, (uint64_t)(timer + dly), bl, bl);
+            s_bus_cont += (uint64_t)(int64_t)db;
+            dly += db;
+        }
+        if (!hit) count(L.off_cnt, cid, 0);
+        dly += L.access_time;
+        int way = set_find(v, L.nways, r.prog);
+        if (way >= 0) {                                      // hit
+            set_ts(v, tsa, way, timer + dly);
+            hit = true;
+            uint32_t st = rl32(v.mst, way);
+            if (r.type == PU_WR) {
+                if constexpr (!kLast) {
+                    if (st != ST_M) {
+                        set_state(v, meta, way, ST_I);
+                        int parent = cid * L.share / g->lv[LV + 1].share;
+                        uint32_t ns = mesi<LV + 1>(parent, r, timer + dly);
+                        set_state(v, meta, way, ns);
+                    }
+                } else {
+                    if (st == ST_S) {
+                        int home = home_of(r.addr);
+                        uint32_t tmp;
+                        dly += (int)transmit(cid, home, 0, (uint64_t)(timer + dly));
+                        dly += access_home(cid, home, r, timer + dly, &tmp);
+                        dly += (int)transmit(home, cid, 0, (uint64_t)(timer + dly));
+                    }
+                    set_state(v, meta, way, ST_M);
+                }
+                return ST_M;
+            }
+            if (st != ST_S) dly += children<LV, false>(cid, r);
+            return ST_S;
+        }
+        // miss
+        uint32_t old_st;
+        uint64_t old_addr;
+        int old_prog;
+        way = set_replace(v, meta, L.nways, L.offbits, L.idxbits, r.prog, &old_st, &old_addr, &old_prog);
+        if (old_st != ST_I) {
+            count(L.off_cnt, cid, 2);
+            Req o{old_addr, old_prog, PU_RD};
+            dly += children<LV, true>(cid, o);
+            if (old_st == ST_M || old_st == ST_E) {
+                count(L.off_cnt, cid, 3);
+                if constexpr (kLast) {                       // write-back; delays discarded (Q3)
+                    int home = home_of(old_addr);
+                    o.type = PU_WB;
+                    uint32_t tmp;
+                    transmit(cid, home, (int)L.block, (uint64_t)(timer + dly));
+                    access_home(cid, home, o, timer + dly, &tmp);
+                }
+            }
+        }
+        set_ts(v, tsa, way, timer + dly);
+        uint32_t res;
+        if constexpr (!kLast) {
+            int parent = cid * L.share / g->lv[LV + 1].share;
+            res = mesi<LV + 1>(parent, r, timer);            // `timer`, not timer+delay (Q2)
+        } else {
+            int home = home_of(r.addr);
+            dly += (int)transmit(cid, home, 0, (uint64_t)(timer + dly));
+            dly += access_home(cid, home, r, timer + dly, &res);
+            dly += (int)transmit(home, cid, (int)L.block, (uint64_t)(timer + dly));
+        }
+        set_state(v, meta, way, res);
+        count(L.off_cnt, cid, 1);
+        return res;
+    }
+
+    // System::access (system.cpp:144-168), directory system, TLB off.
+    __device__ int access(int core, const Req& r, int64_t timer) {
+        if (core < 0 || core >= g->num_cores) {
+            s_err |= PU_ERRF_CORE_RANGE;
+            return -1;
+        }
+        s_reqs++;
+        hit = false;
+        dly = 0;
+        mesi<0>(core, r, timer + dly);
+        return dly;
+    }
+
+    __device__ void flush_stats() {
+        if (ln != 0) return;
+        EngineStats* S = at<EngineStats>(g->off_stats);
+        atomic_add_u64(&S->net_accesses, s_net_acc);
+        atomic_add_u64(&S->net_distance, s_net_dist);
+        atomic_add_u64(&S->net_total_delay, s_net_total);
+        atomic_add_u64(&S->net_router_delay, s_net_router);
+        atomic_add_u64(&S->net_link_delay, s_net_link);
+        atomic_add_u64(&S->net_inject_delay, s_net_inject);
+        atomic_add_u64(&S->dram_accesses, s_dram);
+        atomic_add_u64(&S->total_bus_contention, s_bus_cont);
+        atomic_add_u64(reinterpret_cast<uint64_t*>(&S->total_num_broadcast), (uint64_t)s_bcast);
+        atomic_add_u64(&S->link_flits, s_flits);
+        atomic_add_u64(&S->mg1_calls, s_mg1);
+        atomic_add_u64(&S->lockdown_calls, s_lockdown);
+        atomic_add_u64(&S->bus_accesses, s_busacc);
+        atomic_add_u64(&S->requests, s_reqs);
+        __hip_atomic_fetch_or(&S->error_flags, s_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+};
+
+// One workgroup (= one wavefront) per replica.  Replica replica0 + blockIdx.x
+// processes reqs[off[blockIdx.x] .. off[blockIdx.x+1]) in order: the message
+// loop of prime.cpp:120-137 (D restarts at each batch_start; d = access(core,
+// req, timer + D); D += d - 1).
+template <int NL>
+__global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, char* __restrict__ arena,
+                                                    int replica0, const pu_req* __restrict__ reqs,
+                                                    const uint64_t* __restrict__ off,
+                                                    int32_t* __restrict__ delays) {
+    Engine<NL> e;
+    e.g = g;
+    e.ln = lane_id();
+    e.base = arena + (size_t)(replica0 + (int)blockIdx.x) * g->replica_bytes;
+    e.s_net_acc = e.s_net_dist = e.s_net_total = e.s_net_router = e.s_net_link = e.s_net_inject = 0;
+    e.s_dram = e.s_bus_cont = e.s_flits = e.s_mg1 = e.s_lockdown = e.s_busacc = e.s_reqs = e.s_err = 0;
+    e.s_bcast = 0;
+    e.dly = 0;
+    e.hit = false;
+
+    RunState* rs = e.template at<RunState>(g->off_run);
+    int32_t D = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->batch_delay : 0u, 0);
+    int64_t* completion = e.template at<int64_t>(g->off_completion);
+    const uint64_t b = off[blockIdx.x], end = off[blockIdx.x + 1];
+    for (uint64_t i = b; i < end; i++) {
+        const pu_req q = reqs[i];
+        if (q.batch_start) D = 0;
+        const int64_t t = q.timer + D;
+        Req r{q.addr, q.prog_id, (int32_t)q.mem_type};
+        int d = e.access(q.core, r, t);
+        if (e.ln == 0) {
+            delays[i] = d;
+            if (q.core >= 0 && q.core < g->num_cores) completion[q.core] = t + d;
+        }
+        D += d - 1;
+        if (D < 0) e.s_err |= PU_ERRF_NEG_DELAY;
+    }
+    if (e.ln == 0) {
+        rs->batch_delay = D;
+        rs->processed += end - b;
+    }
+    e.flush_stats();
+}
+
+// Queue records start as the single free interval [0, UINT64_MAX]
+// (QueueModelHistoryTree ctor, queue_model_history_tree.cpp:28).
+__global__ void init_queues_kernel(char* arena, uint64_t replica_bytes, uint64_t off_qhdr, uint64_t off_qring,
+                                   int nqueues, int nreplicas) {
+    uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t total = (uint64_t)nqueues * (uint64_t)nreplicas;
+    if (id >= total) return;
+    uint64_t r = id / (uint64_t)nqueues, q = id % (uint64_t)nqueues;
+    char* base = arena + r * replica_bytes;
+    QueueHdr* h = reinterpret_cast<QueueHdr*>(base + off_qhdr) + q;
+    h->head = 0;
+    h->count = 1;
+    h->n = 0;
+    h->sum = 0.0;
+    h->sum_sq = 0.0;
+    h->newest = 0;
+    QueueSlot* ring = reinterpret_cast<QueueSlot*>(base + off_qring) + q * PU_QRING;
+    ring[0] = QueueSlot{0ull, UINT64_MAX};
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- launchers
+extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,
+                                const pu_req* reqs, const uint64_t* off, int32_t* delays, hipStream_t stream) {
+    dim3 grid((unsigned)nblocks), block(64);
+    switch (num_levels) {
+        case 1: hipLaunchKernelGGL(uncore_kernel<1>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays); break;
+        case 2: hipLaunchKernelGGL(uncore_kernel<2>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays); break;
+        case 3: hipLaunchKernelGGL(uncore_kernel<3>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays); break;
+        case 4: hipLaunchKernelGGL(uncore_kernel<4>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays); break;
+        default: return PU_EINVAL;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : PU_EIO;
+}
+
+extern "C" int pu_engine_init_queues(char* arena, uint64_t replica_bytes, uint64_t off_qhdr, uint64_t off_qring,
+                                     int nqueues, int nreplicas, hipStream_t stream) {
+    uint64_t total = (uint64_t)nqueues * (uint64_t)nreplicas;
+    if (total == 0) return 0;
+    unsigned blocks = (unsigned)((total + 255) / 256);
+    hipLaunchKernelGGL(init_queues_kernel, dim3(blocks), dim3(256), 0, stream, arena, replica_bytes, off_qhdr,
+                       off_qring, nqueues, nreplicas);
+    return hipGetLastError() == hipSuccess ? 0 : PU_EIO;
+}

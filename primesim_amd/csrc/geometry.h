@@ -1,0 +1,97 @@
+// geometry.h — replica memory layout and derived geometry, shared by the
+// host (uncore.cpp) and the HIP engine (engine.hip).
+//
+// One replica = one complete uncore (reference System, system.h:80-130) laid
+// out structure-of-arrays in a single HBM arena:
+//
+//   per data-cache level l (reference Cache, cache.h:102-164):
+//     meta[l]  : ncaches*nsets*nways x LineMeta (16 B: tag, prog id, state)
+//     ts[l]    : ncaches*nsets*nways x int64 LRU timestamps
+//     alive[l] : ncaches x u32 (reference creates caches lazily, system.cpp:172)
+//     cnt[l]   : ncaches x 4 x u64 (ins, miss, evict, wb)
+//   directory / shared-LLC slices (one per network node):
+//     dmeta, dts          : N*nsets*nways lines
+//     dsh                 : N*nsets*nways x nwords x u64 full-map sharer bitmap
+//                           (replaces std::set<int>, iterated in ascending id)
+//     dalive, dcnt        : per slice
+//   queues (Graphite history tree restated as a ring of sorted free intervals):
+//     qhdr : nqueues x QueueHdr (64 B)   — links first, then per-cache buses
+//     qring: nqueues x 128 x {first,second} (2 KB)
+//   stats (EngineStats), per-core completion cycles, run state.
+//
+// Lane ownership inside the wavefront that runs a replica: way w of any set
+// is always read and written by lane w; sharer word k by lane k; queue ring
+// slot s by lane s % 64; every scalar record by lane 0.  Values move between
+// lanes only through registers (readlane / shuffles), so every memory
+// read-after-write is a same-thread program-order dependency.
+#pragma once
+
+#include <stdint.h>
+
+#define PU_QRING 128          // ring capacity (history tree holds <= 100 intervals)
+#define PU_QMAX 100           // QueueModelHistoryTree::_max_free_interval_size
+#define PU_MAX_WAYS 64
+#define PU_MAX_NWORDS 64      // sharer bitmap words -> up to 4096 LLC nodes
+
+struct LineMeta {
+    uint64_t tag;
+    int32_t id;
+    uint32_t state;
+};
+
+struct QueueHdr {
+    uint32_t head;
+    uint32_t count;
+    uint64_t n;        // QueueModelMG1::_num_arrivals
+    double sum;        // _sigma_service_time
+    double sum_sq;     // _sigma_service_time_square
+    uint64_t newest;   // _newest_arrival_time
+    uint64_t _pad[3];
+};
+
+struct QueueSlot {
+    uint64_t first;
+    uint64_t second;
+};
+
+// Accumulated by the kernel (atomic adds at the end of each launch).
+struct EngineStats {
+    uint64_t net_accesses, net_distance, net_total_delay, net_router_delay, net_link_delay,
+        net_inject_delay, dram_accesses, total_bus_contention;
+    int64_t total_num_broadcast;
+    uint64_t link_flits, mg1_calls, lockdown_calls, bus_accesses, requests, error_flags;
+    uint64_t _pad;
+};
+
+struct LevelGeo {
+    uint64_t nsets, nways, block;
+    int32_t offbits, idxbits, access_time, share;
+    int32_t ncaches, nchildren, has_bus, bus_q0;   // bus queue index of cache 0
+    uint64_t off_meta, off_ts, off_alive, off_cnt;
+};
+
+struct DirGeo {
+    uint64_t nsets, nways, block;
+    int32_t offbits, idxbits, access_time, nwords;
+    uint64_t off_meta, off_ts, off_sh, off_alive, off_cnt;
+};
+
+struct Geo {
+    int32_t num_cores, num_levels, sys_type, protocol_type;
+    int32_t max_num_sharers, shared_llc, tlb_enable, dram_access_time;
+    int32_t bus_latency, N, net_type, net_width;
+    int32_t header_flits, data_width, nlinks, nqueues;
+    int32_t home_offbits, home_mask_bits, _pad0, _pad1;
+    uint64_t router_delay, link_delay, inject_delay;
+    LevelGeo lv[4];
+    DirGeo dir;
+    uint64_t off_qhdr, off_qring, off_stats, off_completion, off_run;
+    uint64_t replica_bytes;
+};
+
+// Per-replica run state carried across launches.
+struct RunState {
+    int32_t batch_delay;   // prime.cpp:113 running `delay` of the open message
+    int32_t _pad;
+    uint64_t processed;    // requests processed so far
+};

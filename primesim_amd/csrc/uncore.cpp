@@ -1,0 +1,603 @@
+// uncore.cpp — the C ABI of include/primeuncore.h: engine lifetime, replica
+// layout, the thread->core map, the batch paths that launch the HIP engine,
+// statistics and the report text.
+//
+// Replaces, for the hot path only:
+//   UncoreManager::init/allocCore/deallocCore/getCoreId/uncore_access/report
+//                                   (reference src/uncore_manager.cpp:46-98)
+//   System::init/report             (reference src/system.cpp:47-141, 956-1111)
+//   ThreadSched                     (reference src/thread_sched.cpp:44-118)
+// There is no CPU fallback: without a HIP device pu_create fails (PU_ENODEV).
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/primeuncore.h"
+#include "common.h"
+#include "geometry.h"
+
+extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,
+                                const pu_req* reqs, const uint64_t* off, int32_t* delays, hipStream_t stream);
+extern "C" int pu_engine_init_queues(char* arena, uint64_t replica_bytes, uint64_t off_qhdr, uint64_t off_qring,
+                                     int nqueues, int nreplicas, hipStream_t stream);
+
+namespace pu {
+
+static thread_local std::string g_err;
+
+int set_error(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+}  // namespace pu
+
+namespace {
+
+int ilog2(uint64_t x) { return (int)std::log2((double)x); }
+
+uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+struct Layout {
+    uint64_t cur = 0;
+    uint64_t take(uint64_t bytes, uint64_t align = 256) {
+        cur = align_up(cur, align);
+        uint64_t o = cur;
+        cur += bytes;
+        return o;
+    }
+};
+
+// Validates the configuration (every condition under which the reference
+// is undefined or this engine does not implement the branch) and computes the
+// replica layout.
+int build_geo(const pu_sim_cfg* c, Geo* g) {
+    std::memset(g, 0, sizeof(*g));
+    const pu_sys_cfg& y = c->sys;
+    if (y.num_levels < 1 || y.num_levels > PU_MAX_LEVELS) return pu::set_error(PU_EINVAL, "num_levels must be 1..4");
+    if (y.num_cores < 1) return pu::set_error(PU_EINVAL, "num_cores must be >= 1");
+    if (y.sys_type != 0)
+        return pu::set_error(PU_ENOTSUP, "sys_type=1 (mesi_bus, system.cpp:224) is not implemented by the HIP engine yet");
+    if (y.tlb_enable)
+        return pu::set_error(PU_ENOTSUP, "tlb_enable=1 (system.cpp:897) is not implemented by the HIP engine yet");
+    g->num_cores = y.num_cores;
+    g->num_levels = y.num_levels;
+    g->sys_type = y.sys_type;
+    g->protocol_type = y.protocol_type;
+    g->max_num_sharers = y.max_num_sharers;
+    g->shared_llc = y.shared_llc;
+    g->tlb_enable = y.tlb_enable;
+    g->dram_access_time = y.dram_access_time;
+    g->bus_latency = y.bus_latency;
+    Layout lay;
+    int nbus = 0;
+    for (int l = 0; l < y.num_levels; l++) {
+        const pu_cache_cfg& cc = y.cache[l];
+        LevelGeo& L = g->lv[l];
+        if (cc.share < 1 || cc.block_size < 1 || cc.num_ways < 1) return pu::set_error(PU_EINVAL, "bad cache geometry");
+        if (cc.num_ways > PU_MAX_WAYS) return pu::set_error(PU_ENOTSUP, "at most 64 ways per set");
+        L.nsets = cc.size / (cc.block_size * cc.num_ways);
+        if (L.nsets < 1) return pu::set_error(PU_EINVAL, "cache has no sets");
+        L.nways = cc.num_ways;
+        L.block = cc.block_size;
+        L.offbits = ilog2(cc.block_size);
+        L.idxbits = ilog2(L.nsets);
+        if (L.offbits + L.idxbits >= 64) return pu::set_error(PU_EINVAL, "cache geometry exceeds 64-bit addresses");
+        L.access_time = cc.access_time;
+        L.share = cc.share;
+        L.ncaches = (int)std::ceil((double)y.num_cores / cc.share);
+        L.nchildren = l == 0 ? 0 : cc.share / y.cache[l - 1].share;
+        L.has_bus = cc.share > 1 ? 1 : 0;
+        if (l > 0 && cc.share % y.cache[l - 1].share != 0) return pu::set_error(PU_EINVAL, "cache shares must nest");
+        if (L.has_bus) {
+            if (y.bus_latency < 1) return pu::set_error(PU_EINVAL, "bus_latency must be >= 1 for shared levels");
+            L.bus_q0 = nbus;   // fixed up below (after the link count is known)
+            nbus += L.ncaches;
+        }
+    }
+    if (y.cache[0].share != 1)
+        return pu::set_error(PU_ENOTSUP, "L1 share must be 1 (System::access passes cache[0][core_id], system.cpp:161)");
+    const int N = g->lv[y.num_levels - 1].ncaches;
+    g->N = N;
+    const pu_cache_cfg& dc = y.directory_cache;
+    if (dc.size == 0) return pu::set_error(PU_EINVAL, "a directory is required (system.cpp:1052)");
+    if (dc.num_ways < 1 || dc.block_size < 1) return pu::set_error(PU_EINVAL, "bad directory geometry");
+    if (dc.num_ways > PU_MAX_WAYS) return pu::set_error(PU_ENOTSUP, "at most 64 directory ways");
+    DirGeo& D = g->dir;
+    D.nsets = dc.size / (dc.block_size * dc.num_ways);
+    if (D.nsets < 1) return pu::set_error(PU_EINVAL, "directory has no sets");
+    D.nways = dc.num_ways;
+    D.block = dc.block_size;
+    D.offbits = ilog2(dc.block_size);
+    D.idxbits = ilog2(D.nsets);
+    D.access_time = dc.access_time;
+    D.nwords = (N + 63) / 64;
+    if (D.nwords > PU_MAX_NWORDS) return pu::set_error(PU_ENOTSUP, "at most 4096 LLC nodes");
+    if (y.protocol_type == 1 && N != y.num_cores)
+        return pu::set_error(PU_EINVAL, "limited-pointer broadcast needs one LLC per core (system.cpp:623)");
+    if (y.network.link_delay < 1) return pu::set_error(PU_EINVAL, "link_delay must be >= 1");
+    if (y.network.data_width < 1) return pu::set_error(PU_EINVAL, "data_width must be >= 1");
+    g->home_offbits = ilog2(dc.block_size);
+    g->home_mask_bits = (int)std::ceil(std::log2((double)N));
+    g->net_type = y.network.net_type;
+    g->net_width = g->net_type == 1 ? (int)std::ceil(std::cbrt((double)N)) : (int)std::ceil(std::sqrt((double)N));
+    g->header_flits = y.network.header_flits;
+    g->data_width = y.network.data_width;
+    g->router_delay = y.network.router_delay;
+    g->link_delay = y.network.link_delay;
+    g->inject_delay = y.network.inject_delay;
+    const int w = g->net_width;
+    g->nlinks = w > 1 ? (w - 1) * w * (g->net_type == 1 ? 3 * w : 2) : 0;
+    g->nqueues = g->nlinks + nbus;
+    for (int l = 0; l < y.num_levels; l++)
+        if (g->lv[l].has_bus) g->lv[l].bus_q0 += g->nlinks;
+
+    // ---- layout
+    for (int l = 0; l < y.num_levels; l++) {
+        LevelGeo& L = g->lv[l];
+        uint64_t lines = (uint64_t)L.ncaches * L.nsets * L.nways;
+        L.off_meta = lay.take(lines * sizeof(LineMeta));
+        L.off_ts = lay.take(lines * sizeof(int64_t));
+        L.off_alive = lay.take((uint64_t)L.ncaches * 4);
+        L.off_cnt = lay.take((uint64_t)L.ncaches * 32);
+    }
+    uint64_t dlines = (uint64_t)N * D.nsets * D.nways;
+    D.off_meta = lay.take(dlines * sizeof(LineMeta));
+    D.off_ts = lay.take(dlines * sizeof(int64_t));
+    D.off_sh = lay.take(dlines * (uint64_t)D.nwords * 8);
+    D.off_alive = lay.take((uint64_t)N * 4);
+    D.off_cnt = lay.take((uint64_t)N * 32);
+    g->off_qhdr = lay.take((uint64_t)g->nqueues * sizeof(QueueHdr));
+    g->off_qring = lay.take((uint64_t)g->nqueues * PU_QRING * sizeof(QueueSlot));
+    g->off_stats = lay.take(sizeof(EngineStats));
+    g->off_completion = lay.take((uint64_t)y.num_cores * 8);
+    g->off_run = lay.take(sizeof(RunState));
+    g->replica_bytes = align_up(lay.cur, 4096);
+    return 0;
+}
+
+}  // namespace
+
+struct pu_handle {
+    pu_sim_cfg cfg;
+    Geo geo;
+    Geo* d_geo = nullptr;
+    char* arena = nullptr;
+    int R = 0;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_ms = 0.0;
+    // ThreadSched (thread_sched.cpp): core_stat + ordered (prog, thread) map
+    std::vector<int> core_stat;
+    std::map<std::pair<int, int>, int> core_map;
+    // staging for host-buffer batches
+    pu_req* d_reqs = nullptr;
+    int32_t* d_delays = nullptr;
+    uint64_t* d_off = nullptr;
+    size_t stage_cap = 0;
+    std::mutex mu;
+};
+
+#define HIP_TRY(expr, code)                                                                   \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess) return pu::set_error(code, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+namespace {
+
+int reset_state(pu_handle* h) {
+    HIP_TRY(hipMemsetAsync(h->arena, 0, h->geo.replica_bytes * (size_t)h->R, h->stream), PU_EIO);
+    // completion cycles start at -1 ("no request yet")
+    HIP_TRY(hipMemset2DAsync(h->arena + h->geo.off_completion, h->geo.replica_bytes, 0xFF,
+                             (size_t)h->geo.num_cores * 8, (size_t)h->R, h->stream), PU_EIO);
+    int rc = pu_engine_init_queues(h->arena, h->geo.replica_bytes, h->geo.off_qhdr, h->geo.off_qring,
+                                   h->geo.nqueues, h->R, h->stream);
+    if (rc) return pu::set_error(rc, "queue init launch failed");
+    HIP_TRY(hipStreamSynchronize(h->stream), PU_EIO);
+    return 0;
+}
+
+int ensure_stage(pu_handle* h, size_t n) {
+    if (n <= h->stage_cap && h->d_reqs) return 0;
+    size_t cap = n < 4096 ? 4096 : n;
+    if (h->d_reqs) (void)hipFree(h->d_reqs);
+    if (h->d_delays) (void)hipFree(h->d_delays);
+    h->d_reqs = nullptr;
+    h->d_delays = nullptr;
+    HIP_TRY(hipMalloc(&h->d_reqs, cap * sizeof(pu_req)), PU_ENOMEM);
+    HIP_TRY(hipMalloc(&h->d_delays, cap * sizeof(int32_t)), PU_ENOMEM);
+    if (!h->d_off) HIP_TRY(hipMalloc(&h->d_off, 2 * sizeof(uint64_t)), PU_ENOMEM);
+    h->stage_cap = cap;
+    return 0;
+}
+
+int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
+           hipStream_t s) {
+    HIP_TRY(hipEventRecord(h->ev0, s), PU_EIO);
+    int rc = pu_engine_launch(h->d_geo, h->geo.num_levels, h->arena, replica0, nblocks, d_reqs, d_off, d_delay, s);
+    if (rc) return pu::set_error(rc, "engine launch failed");
+    HIP_TRY(hipEventRecord(h->ev1, s), PU_EIO);
+    return 0;
+}
+
+// Copies replica r's engine-side counters.
+int read_replica(pu_handle* h, int r, EngineStats* es, std::vector<uint64_t> cnt[PU_MAX_LEVELS + 1],
+                 std::vector<uint32_t> alive[PU_MAX_LEVELS + 1]) {
+    const Geo& g = h->geo;
+    char* base = h->arena + (size_t)r * g.replica_bytes;
+    HIP_TRY(hipStreamSynchronize(h->stream), PU_EIO);
+    HIP_TRY(hipMemcpy(es, base + g.off_stats, sizeof(EngineStats), hipMemcpyDeviceToHost), PU_EIO);
+    for (int l = 0; l <= g.num_levels; l++) {
+        bool dir = l == g.num_levels;
+        size_t nc = dir ? (size_t)g.N : (size_t)g.lv[l].ncaches;
+        cnt[l].resize(nc * 4);
+        alive[l].resize(nc);
+        uint64_t oc = dir ? g.dir.off_cnt : g.lv[l].off_cnt;
+        uint64_t oa = dir ? g.dir.off_alive : g.lv[l].off_alive;
+        HIP_TRY(hipMemcpy(cnt[l].data(), base + oc, nc * 32, hipMemcpyDeviceToHost), PU_EIO);
+        HIP_TRY(hipMemcpy(alive[l].data(), base + oa, nc * 4, hipMemcpyDeviceToHost), PU_EIO);
+    }
+    return 0;
+}
+
+// Cache::report (cache.cpp:430-441)
+void cache_report(std::ostream& o, uint64_t size, uint64_t ways, const uint64_t* c) {
+    o << "=================================================================\n";
+    o << "Simulation results for " << size << " Bytes " << ways << "-way set associative cache model:\n";
+    o << "The total # of memory instructions: " << c[0] << std::endl;
+    o << "The # of cache-missed instructions: " << c[1] << std::endl;
+    o << "The # of evicted instructions: " << c[2] << std::endl;
+    o << "The # of writeback instructions: " << c[3] << std::endl;
+    o << "The cache miss rate: " << 100 * (double)c[1] / (double)c[0] << "%" << std::endl;
+    o << "=================================================================\n\n";
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pu_last_error(void) { return pu::g_err.c_str(); }
+const char* pu_version(void) { return "primeuncore 0.1 (gfx950)"; }
+
+pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device) {
+    if (!cfg || num_replicas < 1) {
+        pu::set_error(PU_EINVAL, "bad arguments");
+        return nullptr;
+    }
+    Geo geo;
+    if (build_geo(cfg, &geo) != 0) return nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) {
+        pu::set_error(PU_ENODEV, "no HIP device available (the engine has no CPU fallback)");
+        return nullptr;
+    }
+    pu_handle* h = new pu_handle();
+    h->cfg = *cfg;
+    h->geo = geo;
+    h->R = num_replicas;
+    h->device = device;
+    auto fail = [&](const std::string& m) -> pu_handle* {
+        pu::set_error(PU_ENOMEM, m);
+        pu_destroy(h);
+        return nullptr;
+    };
+    if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice failed");
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream create failed");
+    if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) return fail("event create failed");
+    if (hipMalloc(&h->d_geo, sizeof(Geo)) != hipSuccess) return fail("hipMalloc(geo) failed");
+    if (hipMemcpy(h->d_geo, &geo, sizeof(Geo), hipMemcpyHostToDevice) != hipSuccess) return fail("geo upload failed");
+    size_t bytes = geo.replica_bytes * (size_t)num_replicas;
+    if (hipMalloc(&h->arena, bytes) != hipSuccess) {
+        h->arena = nullptr;
+        return fail("hipMalloc of " + std::to_string(bytes) + " bytes for the replica arena failed");
+    }
+    h->core_stat.assign((size_t)cfg->sys.num_cores, 0);
+    if (reset_state(h) != 0) {
+        std::string m = pu::g_err;
+        pu_destroy(h);
+        pu::set_error(PU_EIO, m);
+        return nullptr;
+    }
+    return h;
+}
+
+void pu_destroy(pu_handle* h) {
+    if (!h) return;
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->arena) (void)hipFree(h->arena);
+    if (h->d_geo) (void)hipFree(h->d_geo);
+    if (h->d_reqs) (void)hipFree(h->d_reqs);
+    if (h->d_delays) (void)hipFree(h->d_delays);
+    if (h->d_off) (void)hipFree(h->d_off);
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int pu_reset(pu_handle* h) {
+    if (!h) return pu::set_error(PU_EINVAL, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    return reset_state(h);
+}
+
+int pu_num_replicas(const pu_handle* h) { return h ? h->R : 0; }
+uint64_t pu_replica_bytes(const pu_handle* h) { return h ? h->geo.replica_bytes : 0; }
+
+int pu_alloc_core(pu_handle* h, int prog_id, int thread_id) {
+    if (!h) return pu::set_error(PU_EINVAL, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    for (size_t i = 0; i < h->core_stat.size(); i++) {
+        if (h->core_stat[i] == 0) {
+            h->core_stat[i] = prog_id;
+            h->core_map[{prog_id, thread_id}] = (int)i;
+            return (int)i;
+        }
+    }
+    return -1;
+}
+
+int pu_get_core_id(pu_handle* h, int prog_id, int thread_id) {
+    if (!h) return pu::set_error(PU_EINVAL, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    return h->core_map[{prog_id, thread_id}];   // operator[]: inserts 0 like the reference
+}
+
+int pu_dealloc_core(pu_handle* h, int prog_id, int thread_id) {
+    if (!h) return pu::set_error(PU_EINVAL, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    int core = h->core_map[{prog_id, thread_id}];
+    if (core >= 0 && core < (int)h->core_stat.size() && h->core_stat[(size_t)core] == 1) {
+        h->core_stat[(size_t)core] = 0;
+        return 1;
+    }
+    return 0;
+}
+
+int pu_access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n, int32_t* delay_out) {
+    if (!h || (!reqs && n)) return pu::set_error(PU_EINVAL, "bad arguments");
+    if (replica < 0 || replica >= h->R) return pu::set_error(PU_ERANGE, "replica out of range");
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> lk(h->mu);
+    int rc = ensure_stage(h, n);
+    if (rc) return rc;
+    uint64_t off[2] = {0, (uint64_t)n};
+    HIP_TRY(hipMemcpyAsync(h->d_reqs, reqs, n * sizeof(pu_req), hipMemcpyHostToDevice, h->stream), PU_EIO);
+    HIP_TRY(hipMemcpyAsync(h->d_off, off, sizeof(off), hipMemcpyHostToDevice, h->stream), PU_EIO);
+    rc = launch(h, replica, 1, h->d_reqs, h->d_off, h->d_delays, h->stream);
+    if (rc) return rc;
+    if (delay_out)
+        HIP_TRY(hipMemcpyAsync(delay_out, h->d_delays, n * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream), PU_EIO);
+    HIP_TRY(hipStreamSynchronize(h->stream), PU_EIO);
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, h->ev0, h->ev1) == hipSuccess) h->last_ms = ms;
+    return 0;
+}
+
+int pu_access(pu_handle* h, int core_id, int prog_id, int mem_type, uint64_t* addr, int64_t timer) {
+    if (!h || !addr) return pu::set_error(PU_EINVAL, "bad arguments");
+    if (core_id >= h->cfg.sys.num_cores) return -1;   // System::access, system.cpp:147-150
+    pu_req r;
+    std::memset(&r, 0, sizeof(r));
+    r.addr = *addr;
+    r.timer = timer;
+    r.core = core_id;
+    r.prog_id = prog_id;
+    r.mem_type = (uint8_t)mem_type;
+    r.batch_start = 1;   // a lone request: running delay 0, `timer` used as given
+    int32_t d = 0;
+    int rc = pu_access_batch(h, 0, &r, 1, &d);
+    if (rc) return rc;
+    return d;
+}
+
+int pu_run_device(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay, void* hip_stream) {
+    if (!h || !d_reqs || !d_off || !d_delay) return pu::set_error(PU_EINVAL, "bad arguments");
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    std::lock_guard<std::mutex> lk(h->mu);
+    return launch(h, 0, h->R, d_reqs, d_off, d_delay, s);
+}
+
+int pu_synchronize(pu_handle* h) {
+    if (!h) return pu::set_error(PU_EINVAL, "null handle");
+    HIP_TRY(hipDeviceSynchronize(), PU_EIO);
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, h->ev0, h->ev1) == hipSuccess) h->last_ms = ms;
+    return 0;
+}
+
+double pu_last_kernel_ms(pu_handle* h) { return h ? h->last_ms : 0.0; }
+
+int pu_core_completion(pu_handle* h, int replica, int64_t* out, size_t n) {
+    if (!h || !out) return pu::set_error(PU_EINVAL, "bad arguments");
+    if (replica < 0 || replica >= h->R) return pu::set_error(PU_ERANGE, "replica out of range");
+    size_t k = n < (size_t)h->geo.num_cores ? n : (size_t)h->geo.num_cores;
+    std::vector<int64_t> tmp((size_t)h->geo.num_cores);
+    char* base = h->arena + (size_t)replica * h->geo.replica_bytes;
+    HIP_TRY(hipStreamSynchronize(h->stream), PU_EIO);
+    HIP_TRY(hipMemcpy(tmp.data(), base + h->geo.off_completion, tmp.size() * 8, hipMemcpyDeviceToHost), PU_EIO);
+    for (size_t i = 0; i < k; i++) out[i] = tmp[i];
+    return 0;
+}
+
+int pu_stats_get(pu_handle* h, int replica, pu_stats* out) {
+    if (!h || !out) return pu::set_error(PU_EINVAL, "bad arguments");
+    if (replica < 0 || replica >= h->R) return pu::set_error(PU_ERANGE, "replica out of range");
+    EngineStats es;
+    std::vector<uint64_t> cnt[PU_MAX_LEVELS + 1];
+    std::vector<uint32_t> alive[PU_MAX_LEVELS + 1];
+    int rc = read_replica(h, replica, &es, cnt, alive);
+    if (rc) return rc;
+    std::memset(out, 0, sizeof(*out));
+    out->net_accesses = es.net_accesses;
+    out->net_distance = es.net_distance;
+    out->net_total_delay = es.net_total_delay;
+    out->net_router_delay = es.net_router_delay;
+    out->net_link_delay = es.net_link_delay;
+    out->net_inject_delay = es.net_inject_delay;
+    out->dram_accesses = es.dram_accesses;
+    out->total_bus_contention = es.total_bus_contention;
+    out->total_num_broadcast = es.total_num_broadcast;
+    out->num_levels = h->geo.num_levels;
+    for (int l = 0; l <= h->geo.num_levels; l++) {
+        pu_level_stats a{0, 0, 0, 0};
+        for (size_t i = 0; i < alive[l].size(); i++) {
+            a.ins += cnt[l][i * 4 + 0];
+            a.miss += cnt[l][i * 4 + 1];
+            a.evict += cnt[l][i * 4 + 2];
+            a.wb += cnt[l][i * 4 + 3];
+        }
+        if (l == h->geo.num_levels) out->directory = a;
+        else out->level[l] = a;
+    }
+    out->link_flits = es.link_flits;
+    out->mg1_calls = es.mg1_calls;
+    out->lockdown_calls = es.lockdown_calls;
+    out->bus_accesses = es.bus_accesses;
+    out->requests = es.requests;
+    out->error_flags = es.error_flags;
+    return 0;
+}
+
+// UncoreManager::report (uncore_manager.cpp:87-98) -> ThreadSched::report
+// (thread_sched.cpp:105-116) -> System::report (system.cpp:956-1111) with
+// Network::report (network.cpp:310-323) and Dram::report (dram.cpp:50-55).
+long pu_report(pu_handle* h, int replica, int include_time, char* buf, size_t cap) {
+    if (!h) return pu::set_error(PU_EINVAL, "null handle");
+    if (replica < 0 || replica >= h->R) return pu::set_error(PU_ERANGE, "replica out of range");
+    EngineStats es;
+    std::vector<uint64_t> cnt[PU_MAX_LEVELS + 1];
+    std::vector<uint32_t> alive[PU_MAX_LEVELS + 1];
+    int rc = read_replica(h, replica, &es, cnt, alive);
+    if (rc) return rc;
+    const Geo& g = h->geo;
+    const pu_sys_cfg& y = h->cfg.sys;
+    std::ostringstream o;
+    o << "*********************************************************\n";
+    o << "*                   PriME Simulator                     *\n";
+    o << "*********************************************************\n\n";
+    if (include_time) o << "Total computation time: " << h->last_ms / 1000.0 << " seconds\n";
+    o << std::endl;
+    o << "Core Allocation:\n";
+    for (const auto& kv : h->core_map)
+        o << "(proc ID: " << kv.first.first << " ,thread ID: " << kv.first.second << ") => "
+          << "core ID: " << kv.second << std::endl;
+    o << std::endl;
+    // Network::report
+    double avg_delay = (double)es.net_total_delay / es.net_accesses;
+    o << "Network Stat:\n";
+    o << "# of accesses: " << es.net_accesses << std::endl;
+    o << "Total network communication distance: " << es.net_distance << std::endl;
+    o << "Total network delay: " << es.net_total_delay << std::endl;
+    o << "Total router delay: " << es.net_router_delay << std::endl;
+    o << "Total link delay: " << es.net_link_delay << std::endl;
+    o << "Total inject delay: " << es.net_inject_delay << std::endl;
+    o << "Total contention delay: " << es.net_link_delay - es.net_distance * y.network.link_delay << std::endl;
+    o << "Average network delay: " << avg_delay << std::endl << std::endl;
+    // Dram::report
+    o << "DRAM Statistics:\n";
+    o << "Total # of DRAM accesses: " << es.dram_accesses << std::endl;
+    o << std::endl << "Simulation result for cache system: \n\n";
+    if (y.verbose_report) {
+        o << "Home Occupation:\n";
+        const int w = g.net_width;
+        if (g.net_type == 1) {
+            o << "Allocated home locations in 3D coordinates:" << std::endl;
+            for (int i = 0; i < g.N; i++)
+                if (alive[g.num_levels][(size_t)i])
+                    o << "(" << (i % (w * w)) % w << ", " << (i % (w * w)) / w << ", " << i / (w * w) << ")\n";
+        } else {
+            o << "Allocated home locations in 2D coordinates:" << std::endl;
+            for (int i = 0; i < g.N; i++)
+                if (alive[g.num_levels][(size_t)i]) o << "(" << i % w << ", " << i / w << ")\n";
+        }
+        o << std::endl;
+    }
+    o << std::endl;
+    o << std::endl;
+    o << "Total delay caused by bus contention: " << es.total_bus_contention << " cycles\n";
+    o << "Total # of broadcast: " << (int)es.total_num_broadcast << "\n\n";
+    for (int i = 0; i < g.num_levels; i++) {
+        uint64_t ins = 0, miss = 0, evict = 0, wb = 0;
+        for (size_t j = 0; j < alive[i].size(); j++) {
+            if (!alive[i][j]) continue;
+            ins += cnt[i][j * 4 + 0];
+            miss += cnt[i][j * 4 + 1];
+            evict += cnt[i][j * 4 + 2];
+            wb += cnt[i][j * 4 + 3];
+        }
+        double miss_rate = (double)miss / (double)ins;
+        o << "LEVEL" << i << "===========================================================\n";
+        o << "Simulation results for " << y.cache[i].size << " Bytes " << y.cache[i].num_ways
+          << "-way set associative cache model:\n";
+        o << "The total # of memory instructions: " << ins << std::endl;
+        o << "The # of cache-missed instructions: " << miss << std::endl;
+        o << "The # of evicted instructions: " << evict << std::endl;
+        o << "The # of writeback instructions: " << wb << std::endl;
+        o << "The cache miss rate: " << 100 * miss_rate << "%" << std::endl;
+        o << "=================================================================\n\n";
+    }
+    {
+        const auto& dc = cnt[g.num_levels];
+        const auto& da = alive[g.num_levels];
+        uint64_t ins = 0, miss = 0, evict = 0;
+        for (size_t j = 0; j < da.size(); j++) {
+            if (!da[j]) continue;
+            ins += dc[j * 4 + 0];
+            miss += dc[j * 4 + 1];
+            evict += dc[j * 4 + 2];
+        }
+        double miss_rate = (double)miss / (double)ins;
+        o << "Directory Cache" << "===========================================================\n";
+        o << "Simulation results for " << y.directory_cache.size << " Bytes " << y.directory_cache.num_ways
+          << "-way set associative cache model:\n";
+        o << "The total # of memory instructions: " << ins << std::endl;
+        o << "The # of cache-missed instructions: " << miss << std::endl;
+        o << "The # of replaced instructions: " << evict << std::endl;
+        o << "The cache miss rate: " << 100 * miss_rate << "%" << std::endl;
+        o << "=================================================================\n\n";
+    }
+    if (y.verbose_report) {
+        o << "Statistics for each cache with non-zero accesses: \n\n";
+        for (int i = 0; i < g.num_levels; i++) {
+            o << "LEVEL" << i << "*****************************************************\n\n";
+            for (size_t j = 0; j < alive[i].size(); j++) {
+                if (alive[i][j] && cnt[i][j * 4] > 0) {
+                    o << "The " << j << "th cache:\n";
+                    cache_report(o, y.cache[i].size, y.cache[i].num_ways, &cnt[i][j * 4]);
+                }
+            }
+            o << "************************************************************\n\n";
+        }
+        o << "****************************************************" << std::endl;
+        o << "Statistics for each directory caches with non-zero accesses" << std::endl;
+        const auto& dc = cnt[g.num_levels];
+        const auto& da = alive[g.num_levels];
+        for (size_t j = 0; j < da.size(); j++) {
+            if (da[j] && dc[j * 4] > 0) {
+                o << "Report for directory cache " << j << std::endl;
+                cache_report(o, y.directory_cache.size, y.directory_cache.num_ways, &dc[j * 4]);
+            }
+        }
+    }
+    std::string s = o.str();
+    if (buf && cap) {
+        size_t k = s.size() < cap - 1 ? s.size() : cap - 1;
+        std::memcpy(buf, s.data(), k);
+        buf[k] = 0;
+    }
+    return (long)s.size();
+}
+
+}  // extern "C"

@@ -1,0 +1,262 @@
+"""Python host mirror of the reference's uncore interface, over the C ABI.
+
+`UncoreManager` follows reference src/uncore_manager.h:51-68 (init, allocCore,
+deallocCore, getCoreId, uncore_access, report) with the same argument meaning
+and error behaviour (uncore_access returns -1 for core_id >= num_cores,
+system.cpp:147-150).  It adds the batch paths the engine is built for:
+`access_batch` (host arrays, one replica) and `run_device` (device-resident
+requests for every replica, the benchmark path).
+
+The HIP library is mandatory: importing works everywhere (stream generation
+and config parsing are host code), but creating an engine without a GPU or
+without the built library raises — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _abi as A
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libprimeuncore.so")
+_lib: Optional[C.CDLL] = None
+
+
+class UncoreError(RuntimeError):
+    pass
+
+
+def lib() -> C.CDLL:
+    """Load libprimeuncore.so (build it with __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise UncoreError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    sig = {
+        "pu_config_load_xml": (C.c_int, [C.c_char_p, P(A.SimCfg)]),
+        "pu_config_parse_xml": (C.c_int, [C.c_char_p, C.c_size_t, P(A.SimCfg)]),
+        "pu_config_write_xml": (C.c_int, [P(A.SimCfg), C.c_char_p, C.c_size_t, P(C.c_size_t)]),
+        "pu_create": (C.c_void_p, [P(A.SimCfg), C.c_int, C.c_int]),
+        "pu_destroy": (None, [C.c_void_p]),
+        "pu_reset": (C.c_int, [C.c_void_p]),
+        "pu_num_replicas": (C.c_int, [C.c_void_p]),
+        "pu_replica_bytes": (C.c_uint64, [C.c_void_p]),
+        "pu_alloc_core": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+        "pu_dealloc_core": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+        "pu_get_core_id": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+        "pu_access": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, P(C.c_uint64), C.c_int64]),
+        "pu_access_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.c_void_p]),
+        "pu_run_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+        "pu_synchronize": (C.c_int, [C.c_void_p]),
+        "pu_core_completion": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
+        "pu_stats_get": (C.c_int, [C.c_void_p, C.c_int, P(A.Stats)]),
+        "pu_report": (C.c_long, [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_size_t]),
+        "pu_last_kernel_ms": (C.c_double, [C.c_void_p]),
+        "pu_last_error": (C.c_char_p, []),
+        "pu_version": (C.c_char_p, []),
+        "pu_stream_count": (C.c_int64, [P(A.StreamParams)]),
+        "pu_stream_generate": (C.c_int64, [P(A.StreamParams), C.c_void_p, C.c_size_t]),
+        "pu_stream_thread_of": (C.c_int, [P(A.StreamParams), C.c_int, P(C.c_int), P(C.c_int)]),
+        "pu_trace_write": (C.c_int, [C.c_char_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    return lib().pu_last_error().decode()
+
+
+# ---------------------------------------------------------------- config
+def load_config(path: str) -> A.SimCfg:
+    """XmlParser::parse equivalent (reference xml_parser.cpp:684)."""
+    cfg = A.SimCfg()
+    rc = lib().pu_config_load_xml(path.encode(), C.byref(cfg))
+    if rc != 0:
+        raise UncoreError(f"config {path}: {last_error()}")
+    return cfg
+
+
+def parse_config(text: str) -> A.SimCfg:
+    cfg = A.SimCfg()
+    b = text.encode()
+    rc = lib().pu_config_parse_xml(b, len(b), C.byref(cfg))
+    if rc != 0:
+        raise UncoreError(f"config: {last_error()}")
+    return cfg
+
+
+def config_from_dict(sim: dict) -> A.SimCfg:
+    from .config import to_xml
+    return parse_config(to_xml(sim))
+
+
+# ---------------------------------------------------------------- streams
+@dataclass
+class StreamSpec:
+    kind: int
+    num_cores: int
+    seed: int = 1
+    quantum: int = 1000
+    num_quanta: int = 1
+    max_msg: int = 100
+    num_progs: int = 1
+    max_requests: int = 0
+    write_pct: int = -1
+
+    def params(self) -> A.StreamParams:
+        return A.StreamParams(self.kind, self.num_cores, self.seed, self.quantum, self.num_quanta,
+                              self.max_msg, self.num_progs, self.max_requests, self.write_pct, 0)
+
+
+def generate_stream(spec: StreamSpec) -> np.ndarray:
+    """Deterministic synthetic request stream in canonical order (REQ_DTYPE)."""
+    p = spec.params()
+    n = lib().pu_stream_count(C.byref(p))
+    if n < 0:
+        raise UncoreError(f"stream: {last_error()} ({n})")
+    out = np.zeros(n, dtype=A.REQ_DTYPE)
+    if n:
+        got = lib().pu_stream_generate(C.byref(p), out.ctypes.data, n)
+        if got != n:
+            raise UncoreError(f"stream generation returned {got}, expected {n}")
+    return out
+
+
+def stream_threads(spec: StreamSpec) -> list[tuple[int, int]]:
+    """(prog_id, thread_id) of every core, in allocation order."""
+    p = spec.params()
+    res = []
+    for c in range(spec.num_cores):
+        pr, th = C.c_int(), C.c_int()
+        if lib().pu_stream_thread_of(C.byref(p), c, C.byref(pr), C.byref(th)) != 0:
+            raise UncoreError(last_error())
+        res.append((pr.value, th.value))
+    return res
+
+
+# ---------------------------------------------------------------- engine
+@dataclass
+class InsMem:
+    """reference src/cache.h:92-99 (the fields System::access reads)."""
+    mem_type: int
+    prog_id: int
+    addr_dmem: int
+    thread_id: int = 0
+    rec_thread_id: int = 0
+
+
+class UncoreManager:
+    """reference UncoreManager (uncore_manager.h:51-68) backed by the HIP engine."""
+
+    def __init__(self) -> None:
+        self._h: Optional[int] = None
+        self.cfg: Optional[A.SimCfg] = None
+        self.replicas = 0
+
+    # UncoreManager::init (uncore_manager.cpp:46-50)
+    def init(self, cfg: A.SimCfg, replicas: int = 1, device: int = 0) -> None:
+        h = lib().pu_create(C.byref(cfg), replicas, device)
+        if not h:
+            raise UncoreError(f"pu_create: {last_error()}")
+        self._h = h
+        self.cfg = cfg
+        self.replicas = replicas
+
+    def close(self) -> None:
+        if self._h:
+            lib().pu_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _handle(self) -> int:
+        if not self._h:
+            raise UncoreError("UncoreManager not initialised")
+        return self._h
+
+    def reset(self) -> None:
+        if lib().pu_reset(self._handle()) != 0:
+            raise UncoreError(last_error())
+
+    @property
+    def replica_bytes(self) -> int:
+        return int(lib().pu_replica_bytes(self._handle()))
+
+    def allocCore(self, prog_id: int, thread_id: int) -> int:
+        return lib().pu_alloc_core(self._handle(), prog_id, thread_id)
+
+    def deallocCore(self, prog_id: int, thread_id: int) -> int:
+        return lib().pu_dealloc_core(self._handle(), prog_id, thread_id)
+
+    def getCoreId(self, prog_id: int, thread_id: int) -> int:
+        return lib().pu_get_core_id(self._handle(), prog_id, thread_id)
+
+    # UncoreManager::uncore_access (uncore_manager.cpp:82-85)
+    def uncore_access(self, core_id: int, ins_mem: InsMem, timer: int) -> int:
+        addr = C.c_uint64(ins_mem.addr_dmem)
+        d = lib().pu_access(self._handle(), core_id, ins_mem.prog_id, ins_mem.mem_type, C.byref(addr), timer)
+        if d < -1:
+            raise UncoreError(f"uncore_access: {last_error()}")
+        ins_mem.addr_dmem = addr.value
+        return d
+
+    def access_batch(self, reqs: np.ndarray, replica: int = 0) -> np.ndarray:
+        """prime.cpp:120-137 for a run of messages; returns per-request delays."""
+        reqs = np.ascontiguousarray(reqs, dtype=A.REQ_DTYPE)
+        out = np.zeros(len(reqs), dtype=np.int32)
+        rc = lib().pu_access_batch(self._handle(), replica, reqs.ctypes.data, len(reqs), out.ctypes.data)
+        if rc != 0:
+            raise UncoreError(f"access_batch: {last_error()}")
+        return out
+
+    def run_device(self, d_reqs_ptr: int, d_off_ptr: int, d_delay_ptr: int, stream_ptr: int = 0) -> None:
+        """All replicas at once on device-resident buffers (asynchronous)."""
+        rc = lib().pu_run_device(self._handle(), d_reqs_ptr, d_off_ptr, d_delay_ptr, stream_ptr or None)
+        if rc != 0:
+            raise UncoreError(f"run_device: {last_error()}")
+
+    def synchronize(self) -> None:
+        if lib().pu_synchronize(self._handle()) != 0:
+            raise UncoreError(last_error())
+
+    def last_kernel_ms(self) -> float:
+        return float(lib().pu_last_kernel_ms(self._handle()))
+
+    def stats(self, replica: int = 0) -> A.Stats:
+        s = A.Stats()
+        if lib().pu_stats_get(self._handle(), replica, C.byref(s)) != 0:
+            raise UncoreError(last_error())
+        return s
+
+    def completion(self, replica: int = 0) -> np.ndarray:
+        n = self.cfg.sys.num_cores
+        out = np.zeros(n, dtype=np.int64)
+        if lib().pu_core_completion(self._handle(), replica, out.ctypes.data, n) != 0:
+            raise UncoreError(last_error())
+        return out
+
+    # UncoreManager::report (uncore_manager.cpp:87-98)
+    def report(self, replica: int = 0, include_time: bool = False) -> str:
+        n = lib().pu_report(self._handle(), replica, int(include_time), None, 0)
+        if n < 0:
+            raise UncoreError(last_error())
+        buf = C.create_string_buffer(n + 1)
+        lib().pu_report(self._handle(), replica, int(include_time), buf, n + 1)
+        return buf.value.decode()
