@@ -1,0 +1,275 @@
+"""Benchmark: simulated memory accesses/s through the uncore at 1024 cores.
+
+Workload (BASELINE.json configs[3]): 1024-core 32x32 mesh,
+private L1 32 KB/8 W + one 256 KB/8 W shared-LLC slice per tile, directory
+MESI (full map), XY links with the Graphite history-tree/M/G/1 model,
+DRAM 120 cycles; synthetic stream: 80% uniform over 2^20 lines + 20% over a
+64-line hotspot, 25% writes, 1-4-cycle gaps, 1000-cycle barriers,
+100-request messages, canonical order.
+
+One "step" = every replica on this GPU advances its own request stream by
+--chunk requests in one engine launch (the hot path: prime.cpp's message loop
+over System::access).  A replica is one complete, independent 1024-core uncore
+(its own seed); the engine runs one replica per wavefront and many replicas
+per GPU, because a single uncore is a strictly sequential fold.
+`value` = all requests processed by all ranks / max-over-ranks wall time of the
+K timed steps, with the requests already resident in HBM.
+
+Rank 0 also times the reference's own CPU uncore (oracle/_ref, compiled from
+/root/reference in the build container) — or, if that library is absent, the
+CPU restatement — on a bounded prefix of replica 0's stream on one host core,
+and checks that the GPU's delays for that prefix are bit-identical.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 under
+torch.distributed.run (one process per GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+METRIC = "simulated memory accesses/sec (uncore) at 1024 cores; % HBM roofline"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def alg_bytes(st: dict, cfg) -> float:
+    """SURVEY.md §8d algorithmic bytes for the counted events."""
+    y = cfg.sys
+    b = 28.0 * st["requests"]
+    for lvl in range(y.num_levels):
+        b += st[f"L{lvl}_ins"] * (16.0 * y.cache[lvl].num_ways + 16.0)
+    n_llc = math.ceil(y.num_cores / y.cache[y.num_levels - 1].share)
+    b += st["directory_ins"] * (16.0 * y.directory_cache.num_ways + 16.0 + 16.0 * math.ceil(n_llc / 64))
+    b += st["net_distance"] * 96.0
+    b += st["dram_accesses"] * 8.0
+    return b
+
+
+def sum_stats(um, replicas: int) -> dict:
+    tot: dict = {}
+    for r in range(replicas):
+        d = um.stats(r).as_dict()
+        for k, v in d.items():
+            if k == "error_flags":
+                tot[k] = tot.get(k, 0) | v
+            elif k != "num_levels":
+                tot[k] = tot.get(k, 0) + v
+    return tot
+
+
+def cpu_baseline(cfg_xml: str, cfg, reqs: np.ndarray, threads, budget_s: float):
+    """Time the reference CPU uncore (or the restatement) on a prefix of `reqs`."""
+    import oracle as O
+    kind = "reference" if O.ref_available() else "port"
+    eng = O.RefUncore(cfg_xml) if kind == "reference" else O.CpuRef(cfg)
+    for prog, th in threads:
+        eng.alloc_core(prog, th)
+    chunk = 5000
+    done = 0
+    delays = []
+    t0 = time.perf_counter()
+    while done < len(reqs) and time.perf_counter() - t0 < budget_s:
+        d, rc = eng.run(reqs[done:done + chunk])
+        delays.append(d)
+        done += len(d)
+    el = time.perf_counter() - t0
+    return kind, done, el, np.concatenate(delays) if delays else np.zeros(0, np.int32)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--replicas", type=int, default=0, help="replicas per GPU (0 = size to HBM)")
+    ap.add_argument("--chunk", type=int, default=2500, help="requests per replica per step")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import primesim_amd as P
+    from primesim_amd import _abi as A
+    from primesim_amd import config as CF
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    sim = CF.preset("C4")
+    xml_path = os.path.join(tempfile.gettempdir(), f"pu_bench_c4_{os.getpid()}.xml")
+    CF.write_xml(sim, xml_path)
+    cfg = P.load_config(xml_path)
+
+    # ---- size the replica count to HBM (one replica ~= 0.65 GB at C4)
+    um = P.UncoreManager()
+    probe = P.UncoreManager()
+    probe.init(cfg, replicas=1, device=local)
+    rbytes = probe.replica_bytes
+    probe.close()
+    free, total = torch.cuda.mem_get_info(dev)
+    R = args.replicas or max(1, min(512, int((free * 0.85) // rbytes)))
+    R = max(1, R - R % 8) if R >= 8 else R
+    log(f"[bench] rank {rank}: replica {rbytes / 2**20:.0f} MiB, {R} replicas, free {free / 2**30:.0f} GiB")
+    um.init(cfg, replicas=R, device=local)
+
+    # ---- request streams (one seed per replica, disjoint across ranks), resident in HBM
+    per = args.chunk * (args.warmup + args.steps)
+    streams = []
+    t_gen = time.time()
+    for r in range(R):
+        spec = P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=4 + 1000 * rank + r, num_quanta=64,
+                            max_requests=per)
+        s = P.generate_stream(spec)
+        assert len(s) == per, (len(s), per)
+        streams.append(s)
+    threads = P.stream_threads(P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024))
+    for prog, th in threads:
+        um.allocCore(prog, th)
+    host = np.stack(streams)                       # [R, per] requests
+    log(f"[bench] generated {host.size} requests in {time.time() - t_gen:.1f}s")
+    # step-major layout so each launch reads one contiguous slab: [steps][R][chunk]
+    nsteps = args.warmup + args.steps
+    slab = host.reshape(R, nsteps, args.chunk).transpose(1, 0, 2).copy()
+    d_reqs = torch.from_numpy(slab.view(np.uint8).reshape(-1)).to(dev)
+    d_delay = torch.zeros(nsteps * R * args.chunk, dtype=torch.int32, device=dev)
+    offs = []
+    for s in range(nsteps):
+        o = (np.arange(R + 1, dtype=np.uint64) * args.chunk) + np.uint64(s * R * args.chunk)
+        offs.append(torch.from_numpy(o.astype(np.uint64).view(np.int64)).to(dev))
+    # a dedicated (non-null) stream: the engine launches on it and the HIP
+    # events below time exactly those launches
+    stream = torch.cuda.Stream(dev)
+    sptr = stream.cuda_stream
+    assert sptr != 0
+
+    def launch(s: int) -> None:
+        um.run_device(d_reqs.data_ptr(), offs[s].data_ptr(), d_delay.data_ptr(), sptr)
+
+    for s in range(args.warmup):
+        launch(s)
+        torch.cuda.synchronize(dev)
+        log(f"[bench] warmup step {s} done")
+    before = sum_stats(um, R)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        launch(args.warmup + k)
+        ev[k][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    log(f"[bench] timed {args.steps} steps in {elapsed:.3f}s; per-launch ms {['%.1f' % x for x in kern_ms]}")
+
+    after = sum_stats(um, R)
+    delta = {k: after[k] - before.get(k, 0) for k in after if k != "error_flags"}
+    errf = after.get("error_flags", 0)
+    processed = R * args.chunk * args.steps
+    t_max = elapsed
+    tot_processed = processed
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_max = float(t.item())
+        n = torch.tensor([processed], dtype=torch.int64, device=dev)
+        dist.all_reduce(n, op=dist.ReduceOp.SUM)
+        tot_processed = int(n.item())
+    value = tot_processed / t_max
+
+    # ---- roofline of the engine kernel (per launch, this rank)
+    avg_ms = float(np.mean(kern_ms))
+    bytes_per_launch = alg_bytes(delta, cfg) / args.steps
+    achieved = bytes_per_launch / (avg_ms / 1e3) / 1e9
+
+    result = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu:
+            # replica 0's stream, long enough for a time-bounded (~cpu_seconds) sample
+            long0 = P.generate_stream(P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=4, num_quanta=64,
+                                                   max_requests=max(per, 2_000_000)))
+            assert np.array_equal(long0[:per], streams[0])
+            kind, n_cpu, el, d_cpu = cpu_baseline(xml_path, cfg, long0, threads, args.cpu_seconds)
+            # bit-exact check of replica 0's GPU delays on the same prefix
+            gpu_d = d_delay.cpu().numpy().reshape(nsteps, R, args.chunk)[:, 0, :].reshape(-1)
+            m = min(len(d_cpu), len(gpu_d))
+            parity = bool(np.array_equal(gpu_d[:m], d_cpu[:m]))
+            cpu = {"value": n_cpu / el, "unit": "accesses/s", "cores": 1, "kind": kind,
+                   "sample": f"first {n_cpu} requests of replica 0's C4 stream, single-threaded "
+                             f"({'reference uncore compiled from /root/reference/src' if kind == 'reference' else 'oracle/cpu_ref restatement'}), "
+                             f"{el:.1f} s; GPU delays bit-identical on that prefix: {parity} ({m} compared)"}
+            log(f"[bench] cpu baseline ({kind}): {n_cpu / el:.0f} accesses/s; parity on {m} delays: {parity}")
+        result = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "accesses/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic",
+            "config": {
+                "workload": "C4: 1024-core 32x32 mesh, L1 32KB/8W + 256KB/8W shared-LLC slice per tile, "
+                            "directory MESI full-map, uniform 2^20 lines + 64-line hotspot, 25% writes",
+                "replicas_per_gpu": R,
+                "requests_per_replica_per_step": args.chunk,
+                "parallelism": f"replicas: {R} independent uncores per GPU x {world} GPU(s)",
+                "per_replica_accesses_per_s": value / (R * world),
+                "error_flags": errf,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "kernel": "uncore_kernel<1>",
+                "avg_launch_ms": avg_ms,
+                "alg_bytes_per_launch": bytes_per_launch,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    um.close()
+    try:
+        os.remove(xml_path)
+    except OSError:
+        pass
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

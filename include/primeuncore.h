@@ -275,6 +275,22 @@ int pu_stream_thread_of(const pu_stream_params* p, int core, int* prog_id, int* 
 int pu_trace_write(const char* path, const pu_req* reqs, size_t n,
                    const int32_t* thread_prog, const int32_t* thread_id, int num_threads);
 
+/* ------------------------------------------------------------------------
+ * Unit hooks: run one engine component alone on the GPU (one wavefront), for
+ * the component-level parity tests.
+ * ---------------------------------------------------------------------- */
+/* QueueModelHistoryTree::computeQueueDelay sequence on a fresh queue
+ * (queue_model_history_tree.cpp:42-125 + queue_model_m_g_1.cpp). */
+int pu_unit_queue_run(uint64_t min_proc, const uint64_t* t, const uint64_t* p, size_t n,
+                      uint64_t* delay_out, uint64_t* mg1_calls, int device);
+/* Network::transmit sequence on a fresh mesh (network.cpp:97-160); st gets
+ * the network counters. */
+int pu_unit_network_run(int num_nodes, int net_type, int data_width, int header_flits,
+                        uint64_t router_delay, uint64_t link_delay, uint64_t inject_delay,
+                        const int32_t* src, const int32_t* dst, const int32_t* len,
+                        const uint64_t* timer, size_t n, uint64_t* delay_out, pu_stats* st,
+                        int device);
+
 #ifdef __cplusplus
 }
 #endif

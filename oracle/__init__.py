@@ -46,6 +46,9 @@ def oracle_lib() -> C.CDLL:
         L.cpuref_cache_counters.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]
         L.cpuref_queue_run.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
                                        P(C.c_uint64)]
+        L.cpuref_network_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64,
+                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                         P(A.Stats)]
         _olib = L
     return _olib
 
@@ -133,6 +136,20 @@ def cpuref_queue(min_proc: int, t: np.ndarray, p: np.ndarray) -> tuple[np.ndarra
     calls = C.c_uint64(0)
     oracle_lib().cpuref_queue_run(min_proc, t.ctypes.data, p.ctypes.data, len(t), out.ctypes.data, C.byref(calls))
     return out, int(calls.value)
+
+
+def cpuref_network(nodes: int, net_type: int, data_width: int, header_flits: int, router_delay: int,
+                   link_delay: int, inject_delay: int, src, dst, ln, timer) -> tuple[np.ndarray, A.Stats]:
+    src = np.ascontiguousarray(src, dtype=np.int32)
+    dst = np.ascontiguousarray(dst, dtype=np.int32)
+    ln = np.ascontiguousarray(ln, dtype=np.int32)
+    timer = np.ascontiguousarray(timer, dtype=np.uint64)
+    out = np.zeros(len(src), dtype=np.uint64)
+    st = A.Stats()
+    oracle_lib().cpuref_network_run(nodes, net_type, data_width, header_flits, router_delay, link_delay,
+                                    inject_delay, src.ctypes.data, dst.ctypes.data, ln.ctypes.data,
+                                    timer.ctypes.data, len(src), out.ctypes.data, C.byref(st))
+    return out, st
 
 
 REF_COUNTER_NAMES = ("link_visits", "link_flits", "mg1_calls", "lockdown_calls", "bus_accesses",

@@ -214,6 +214,7 @@ struct Sys {
     std::vector<int> core_stat;
     std::map<std::pair<int, int>, int> core_map;
     std::vector<int64_t> completion;
+    int batch_delay = 0;   // running delay of the open message, kept across cpuref_run calls
 
     // -------------------------------------------------- geometry
     std::string init(const pu_sim_cfg* c) {
@@ -846,7 +847,7 @@ int cpuref_alloc_core(void* h, int prog, int thread) {
 
 long cpuref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
     Sys* s = (Sys*)h;
-    int delay = 0;
+    int delay = s->batch_delay;
     for (size_t i = 0; i < n; i++) {
         const pu_req& q = reqs[i];
         if (q.batch_start) delay = 0;
@@ -857,9 +858,11 @@ long cpuref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
         if (q.core >= 0 && q.core < s->cores) s->completion[(size_t)q.core] = t + d;
         if (delay < 0) {
             s->st.error_flags |= PU_ERRF_NEG_DELAY;
+            s->batch_delay = delay;
             return (long)i + 1;
         }
     }
+    s->batch_delay = delay;
     return 0;
 }
 
@@ -886,6 +889,26 @@ int cpuref_cache_counters(void* h, int level, uint64_t* out, size_t n) {
         out[k++] = c.ins; out[k++] = c.miss; out[k++] = c.evict; out[k++] = c.wb;
     }
     return (int)(k / 4);
+}
+
+int cpuref_network_run(int num_nodes, int net_type, int data_width, int header_flits, uint64_t router_delay,
+                       uint64_t link_delay, uint64_t inject_delay, const int32_t* src, const int32_t* dst,
+                       const int32_t* len, const uint64_t* timer, size_t n, uint64_t* delay_out, pu_stats* st) {
+    Sys s;
+    std::memset(&s.st, 0, sizeof(s.st));
+    s.N = num_nodes;
+    s.net_type = net_type;
+    s.w = net_type == 1 ? (int)std::ceil(std::cbrt((double)num_nodes)) : (int)std::ceil(std::sqrt((double)num_nodes));
+    s.header_flits = header_flits;
+    s.data_width = data_width;
+    s.router = router_delay;
+    s.link_delay = link_delay;
+    s.inject = inject_delay;
+    size_t nl = s.w > 1 ? (size_t)(s.w - 1) * (size_t)s.w * (net_type == 1 ? 3 * (size_t)s.w : 2) : 0;
+    s.links.resize(nl);
+    for (size_t i = 0; i < n; i++) delay_out[i] = s.transmit(src[i], dst[i], len[i], timer[i]);
+    if (st) *st = s.st;
+    return 0;
 }
 
 int cpuref_queue_run(uint64_t min_proc, const uint64_t* t, const uint64_t* p, size_t n,

@@ -26,6 +26,12 @@ int cpuref_completion(void* h, int64_t* out, size_t n);
  * directory slices; out holds ncaches*4 entries (ins, miss, evict, wb). */
 int cpuref_cache_counters(void* h, int level, uint64_t* out, size_t n);
 
+/* Network::transmit sequence on a fresh mesh (network.cpp:97-160); st gets
+ * the network counters. */
+int cpuref_network_run(int num_nodes, int net_type, int data_width, int header_flits, uint64_t router_delay,
+                       uint64_t link_delay, uint64_t inject_delay, const int32_t* src, const int32_t* dst,
+                       const int32_t* len, const uint64_t* timer, size_t n, uint64_t* delay_out, pu_stats* st);
+
 /* Graphite history-tree queue model alone: min_proc, (t_i, p_i) -> delay_i. */
 int cpuref_queue_run(uint64_t min_proc, const uint64_t* t, const uint64_t* p, size_t n,
                      uint64_t* delay_out, uint64_t* mg1_calls);

@@ -76,6 +76,7 @@ struct RefInstance {
     System sys;
     ThreadSched sched;
     int num_cores = 0;
+    int batch_delay = 0;   // prime.cpp's running `delay` of the open message, kept across calls
     std::vector<int64_t> completion;
 };
 
@@ -150,7 +151,7 @@ int ref_get_core_id(void* h, int prog, int thread) {
 // negative (prime.cpp:130 would kill the handler thread there).
 long ref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
     RefInstance* r = (RefInstance*)h;
-    int delay = 0;   // prime.cpp:113 `delay` is an int
+    int delay = r->batch_delay;   // prime.cpp:113 `delay` is an int
     InsMem ins;
     std::memset(&ins, 0, sizeof(ins));
     for (size_t i = 0; i < n; i++) {
@@ -164,8 +165,12 @@ long ref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
         if (delays) delays[i] = d;
         delay += d - 1;
         if (q.core >= 0 && q.core < r->num_cores) r->completion[(size_t)q.core] = t + d;
-        if (delay < 0) return (long)i + 1;
+        if (delay < 0) {
+            r->batch_delay = delay;
+            return (long)i + 1;
+        }
     }
+    r->batch_delay = delay;
     return 0;
 }
 

@@ -840,7 +840,60 @@ __global__ void init_queues_kernel(char* arena, uint64_t replica_bytes, uint64_t
     ring[0] = QueueSlot{0ull, UINT64_MAX};
 }
 
+// ---- unit-test hooks: the queue model / the network alone, one wavefront
+__global__ __launch_bounds__(64) void unit_queue_kernel(const Geo* __restrict__ g, char* base, uint64_t minp,
+                                                        const uint64_t* __restrict__ t,
+                                                        const uint64_t* __restrict__ p, uint64_t n,
+                                                        uint64_t* __restrict__ out, uint64_t* __restrict__ mg1) {
+    Engine<1> e;
+    e.g = g;
+    e.ln = lane_id();
+    e.base = base;
+    e.s_mg1 = 0;
+    e.s_err = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        QueueView v;
+        e.q_issue(v, 0);
+        uint64_t d = e.q_apply(v, 0, t[i], p[i], minp);
+        if (e.ln == 0) out[i] = d;
+    }
+    if (e.ln == 0) *mg1 = e.s_mg1;
+}
+
+__global__ __launch_bounds__(64) void unit_network_kernel(const Geo* __restrict__ g, char* base,
+                                                          const int32_t* __restrict__ src,
+                                                          const int32_t* __restrict__ dst,
+                                                          const int32_t* __restrict__ len,
+                                                          const uint64_t* __restrict__ timer, uint64_t n,
+                                                          uint64_t* __restrict__ out) {
+    Engine<1> e;
+    e.g = g;
+    e.ln = lane_id();
+    e.base = base;
+    e.s_net_acc = e.s_net_dist = e.s_net_total = e.s_net_router = e.s_net_link = e.s_net_inject = 0;
+    e.s_dram = e.s_bus_cont = e.s_flits = e.s_mg1 = e.s_lockdown = e.s_busacc = e.s_reqs = e.s_err = 0;
+    e.s_bcast = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t d = e.transmit(src[i], dst[i], len[i], timer[i]);
+        if (e.ln == 0) out[i] = d;
+    }
+    e.flush_stats();
+}
+
 }  // namespace
+
+extern "C" int pu_engine_unit_queue(const Geo* d_geo, char* base, uint64_t minp, const uint64_t* t,
+                                    const uint64_t* p, uint64_t n, uint64_t* out, uint64_t* mg1, hipStream_t s) {
+    hipLaunchKernelGGL(unit_queue_kernel, dim3(1), dim3(64), 0, s, d_geo, base, minp, t, p, n, out, mg1);
+    return hipGetLastError() == hipSuccess ? 0 : PU_EIO;
+}
+
+extern "C" int pu_engine_unit_network(const Geo* d_geo, char* base, const int32_t* src, const int32_t* dst,
+                                      const int32_t* len, const uint64_t* timer, uint64_t n, uint64_t* out,
+                                      hipStream_t s) {
+    hipLaunchKernelGGL(unit_network_kernel, dim3(1), dim3(64), 0, s, d_geo, base, src, dst, len, timer, n, out);
+    return hipGetLastError() == hipSuccess ? 0 : PU_EIO;
+}
 
 // ---------------------------------------------------------------- launchers
 extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,

@@ -27,6 +27,11 @@
 
 extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,
                                 const pu_req* reqs, const uint64_t* off, int32_t* delays, hipStream_t stream);
+extern "C" int pu_engine_unit_queue(const Geo* d_geo, char* base, uint64_t minp, const uint64_t* t,
+                                    const uint64_t* p, uint64_t n, uint64_t* out, uint64_t* mg1, hipStream_t s);
+extern "C" int pu_engine_unit_network(const Geo* d_geo, char* base, const int32_t* src, const int32_t* dst,
+                                      const int32_t* len, const uint64_t* timer, uint64_t n, uint64_t* out,
+                                      hipStream_t s);
 extern "C" int pu_engine_init_queues(char* arena, uint64_t replica_bytes, uint64_t off_qhdr, uint64_t off_qring,
                                      int nqueues, int nreplicas, hipStream_t stream);
 
@@ -598,6 +603,131 @@ long pu_report(pu_handle* h, int replica, int include_time, char* buf, size_t ca
         buf[k] = 0;
     }
     return (long)s.size();
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- unit hooks
+namespace {
+
+// RAII bag of device buffers for the unit hooks.
+struct DevBufs {
+    std::vector<void*> ptrs;
+    ~DevBufs() {
+        for (void* p : ptrs) (void)hipFree(p);
+    }
+    template <class T>
+    T* up(const T* host, size_t n) {
+        void* d = nullptr;
+        if (hipMalloc(&d, n * sizeof(T) + 8) != hipSuccess) return nullptr;
+        ptrs.push_back(d);
+        if (host && n && hipMemcpy(d, host, n * sizeof(T), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+        return (T*)d;
+    }
+};
+
+int unit_prepare(int device) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev)
+        return pu::set_error(PU_ENODEV, "no HIP device available");
+    HIP_TRY(hipSetDevice(device), PU_ENODEV);
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pu_unit_queue_run(uint64_t min_proc, const uint64_t* t, const uint64_t* p, size_t n, uint64_t* delay_out,
+                      uint64_t* mg1_calls, int device) {
+    if ((!t || !p || !delay_out) && n) return pu::set_error(PU_EINVAL, "bad arguments");
+    int rc = unit_prepare(device);
+    if (rc) return rc;
+    Geo g;
+    std::memset(&g, 0, sizeof(g));
+    g.off_qhdr = 0;
+    g.off_qring = 256;
+    g.nqueues = 1;
+    g.replica_bytes = 256 + PU_QRING * sizeof(QueueSlot);
+    DevBufs b;
+    Geo* dg = b.up(&g, 1);
+    char* base = b.up<char>(nullptr, g.replica_bytes);
+    uint64_t* dt = b.up(t, n);
+    uint64_t* dp = b.up(p, n);
+    uint64_t* dout = b.up<uint64_t>(nullptr, n);
+    uint64_t* dmg = b.up<uint64_t>(nullptr, 1);
+    if (!dg || !base || !dt || !dp || !dout || !dmg) return pu::set_error(PU_ENOMEM, "unit buffers");
+    HIP_TRY(hipMemset(base, 0, g.replica_bytes), PU_EIO);
+    rc = pu_engine_init_queues(base, g.replica_bytes, g.off_qhdr, g.off_qring, 1, 1, nullptr);
+    if (rc) return pu::set_error(rc, "queue init failed");
+    rc = pu_engine_unit_queue(dg, base, min_proc, dt, dp, n, dout, dmg, nullptr);
+    if (rc) return pu::set_error(rc, "unit queue launch failed");
+    HIP_TRY(hipDeviceSynchronize(), PU_EIO);
+    if (n) HIP_TRY(hipMemcpy(delay_out, dout, n * 8, hipMemcpyDeviceToHost), PU_EIO);
+    if (mg1_calls) HIP_TRY(hipMemcpy(mg1_calls, dmg, 8, hipMemcpyDeviceToHost), PU_EIO);
+    return 0;
+}
+
+int pu_unit_network_run(int num_nodes, int net_type, int data_width, int header_flits, uint64_t router_delay,
+                        uint64_t link_delay, uint64_t inject_delay, const int32_t* src, const int32_t* dst,
+                        const int32_t* len, const uint64_t* timer, size_t n, uint64_t* delay_out, pu_stats* st,
+                        int device) {
+    if ((!src || !dst || !len || !timer || !delay_out) && n) return pu::set_error(PU_EINVAL, "bad arguments");
+    if (num_nodes < 1 || data_width < 1 || link_delay < 1) return pu::set_error(PU_EINVAL, "bad network");
+    for (size_t i = 0; i < n; i++)
+        if (src[i] < 0 || src[i] >= num_nodes || dst[i] < 0 || dst[i] >= num_nodes)
+            return pu::set_error(PU_ERANGE, "node id out of range");
+    int rc = unit_prepare(device);
+    if (rc) return rc;
+    Geo g;
+    std::memset(&g, 0, sizeof(g));
+    g.N = num_nodes;
+    g.net_type = net_type;
+    g.net_width = net_type == 1 ? (int)std::ceil(std::cbrt((double)num_nodes)) : (int)std::ceil(std::sqrt((double)num_nodes));
+    g.header_flits = header_flits;
+    g.data_width = data_width;
+    g.router_delay = router_delay;
+    g.link_delay = link_delay;
+    g.inject_delay = inject_delay;
+    const int w = g.net_width;
+    g.nlinks = w > 1 ? (w - 1) * w * (net_type == 1 ? 3 * w : 2) : 0;
+    g.nqueues = g.nlinks;
+    Layout lay;
+    g.off_qhdr = lay.take((uint64_t)g.nqueues * sizeof(QueueHdr));
+    g.off_qring = lay.take((uint64_t)g.nqueues * PU_QRING * sizeof(QueueSlot));
+    g.off_stats = lay.take(sizeof(EngineStats));
+    g.replica_bytes = align_up(lay.cur, 4096);
+    DevBufs b;
+    Geo* dg = b.up(&g, 1);
+    char* base = b.up<char>(nullptr, g.replica_bytes);
+    int32_t* ds = b.up(src, n);
+    int32_t* dd = b.up(dst, n);
+    int32_t* dl = b.up(len, n);
+    uint64_t* dt = b.up(timer, n);
+    uint64_t* dout = b.up<uint64_t>(nullptr, n);
+    if (!dg || !base || !ds || !dd || !dl || !dt || !dout) return pu::set_error(PU_ENOMEM, "unit buffers");
+    HIP_TRY(hipMemset(base, 0, g.replica_bytes), PU_EIO);
+    rc = pu_engine_init_queues(base, g.replica_bytes, g.off_qhdr, g.off_qring, g.nqueues, 1, nullptr);
+    if (rc) return pu::set_error(rc, "queue init failed");
+    rc = pu_engine_unit_network(dg, base, ds, dd, dl, dt, n, dout, nullptr);
+    if (rc) return pu::set_error(rc, "unit network launch failed");
+    HIP_TRY(hipDeviceSynchronize(), PU_EIO);
+    if (n) HIP_TRY(hipMemcpy(delay_out, dout, n * 8, hipMemcpyDeviceToHost), PU_EIO);
+    if (st) {
+        EngineStats es;
+        HIP_TRY(hipMemcpy(&es, base + g.off_stats, sizeof(es), hipMemcpyDeviceToHost), PU_EIO);
+        std::memset(st, 0, sizeof(*st));
+        st->net_accesses = es.net_accesses;
+        st->net_distance = es.net_distance;
+        st->net_total_delay = es.net_total_delay;
+        st->net_router_delay = es.net_router_delay;
+        st->net_link_delay = es.net_link_delay;
+        st->net_inject_delay = es.net_inject_delay;
+        st->link_flits = es.link_flits;
+        st->mg1_calls = es.mg1_calls;
+        st->error_flags = es.error_flags;
+    }
+    return 0;
 }
 
 }  // extern "C"

@@ -1,0 +1,30 @@
+"""Multi-GPU plumbing for the replica engine (one process per GPU).
+
+The uncore of one simulated system is a strictly sequential fold,
+so N GPUs run disjoint sets of independent replicas: no collective on the data
+path.  The only cross-rank operations are the benchmark's barrier and the
+reduction of its timing and request counts (max over ranks of the elapsed
+time, sum of requests processed) — both here so they can be exercised with
+the gloo backend on CPU.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def replica_seed(base: int, rank: int, replica: int) -> int:
+    """Seed of replica `replica` on `rank`: disjoint across ranks and replicas."""
+    return base + 1000 * rank + replica
+
+
+def reduce_run(elapsed_s: float, processed: int, device: torch.device | None = None) -> tuple[float, int]:
+    """(max elapsed over ranks, total requests over ranks); identity when not distributed."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return elapsed_s, processed
+    dev = device if device is not None else torch.device("cpu")
+    t = torch.tensor([elapsed_s], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    n = torch.tensor([processed], dtype=torch.int64, device=dev)
+    dist.all_reduce(n, op=dist.ReduceOp.SUM)
+    return float(t.item()), int(n.item())

@@ -66,6 +66,11 @@ def lib() -> C.CDLL:
         "pu_stream_generate": (C.c_int64, [P(A.StreamParams), C.c_void_p, C.c_size_t]),
         "pu_stream_thread_of": (C.c_int, [P(A.StreamParams), C.c_int, P(C.c_int), P(C.c_int)]),
         "pu_trace_write": (C.c_int, [C.c_char_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int]),
+        "pu_unit_queue_run": (C.c_int, [C.c_uint64, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                        P(C.c_uint64), C.c_int]),
+        "pu_unit_network_run": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64,
+                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                          P(A.Stats), C.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -260,3 +265,34 @@ class UncoreManager:
         buf = C.create_string_buffer(n + 1)
         lib().pu_report(self._handle(), replica, int(include_time), buf, n + 1)
         return buf.value.decode()
+
+
+# ---------------------------------------------------------------- unit hooks
+def unit_queue(min_proc: int, t: np.ndarray, p: np.ndarray, device: int = 0) -> tuple[np.ndarray, int]:
+    """The history-tree queue model alone on the GPU."""
+    t = np.ascontiguousarray(t, dtype=np.uint64)
+    p = np.ascontiguousarray(p, dtype=np.uint64)
+    out = np.zeros(len(t), dtype=np.uint64)
+    calls = C.c_uint64(0)
+    rc = lib().pu_unit_queue_run(min_proc, t.ctypes.data, p.ctypes.data, len(t), out.ctypes.data, C.byref(calls),
+                                 device)
+    if rc != 0:
+        raise UncoreError(f"unit_queue: {last_error()}")
+    return out, int(calls.value)
+
+
+def unit_network(nodes: int, net_type: int, data_width: int, header_flits: int, router_delay: int,
+                 link_delay: int, inject_delay: int, src, dst, ln, timer, device: int = 0):
+    """Network::transmit sequence alone on the GPU."""
+    src = np.ascontiguousarray(src, dtype=np.int32)
+    dst = np.ascontiguousarray(dst, dtype=np.int32)
+    ln = np.ascontiguousarray(ln, dtype=np.int32)
+    timer = np.ascontiguousarray(timer, dtype=np.uint64)
+    out = np.zeros(len(src), dtype=np.uint64)
+    st = A.Stats()
+    rc = lib().pu_unit_network_run(nodes, net_type, data_width, header_flits, router_delay, link_delay,
+                                   inject_delay, src.ctypes.data, dst.ctypes.data, ln.ctypes.data,
+                                   timer.ctypes.data, len(src), out.ctypes.data, C.byref(st), device)
+    if rc != 0:
+        raise UncoreError(f"unit_network: {last_error()}")
+    return out, st

@@ -1,0 +1,74 @@
+"""The C-ABI library: loads, exports every symbol include/primeuncore.h declares,
+validates configurations before touching a device, and fails loudly (no CPU
+fallback) where there is no GPU."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+import primesim_amd as P
+from primesim_amd import config as CF
+from primesim_amd.uncore import lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    with open(os.path.join(ROOT, "include", "primeuncore.h")) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^[A-Za-z_][\w \*]*?\b(pu_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_exports_every_declared_symbol():
+    syms = declared_symbols()
+    assert len(syms) >= 25
+    L = lib()
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+
+
+def test_version_and_error_strings():
+    assert b"gfx950" in lib().pu_version()
+    assert isinstance(P.uncore.last_error(), str)
+
+
+def _gpu_present() -> bool:
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.mark.skipif(_gpu_present(), reason="checks the no-GPU path")
+def test_no_gpu_fails_loudly():
+    um = P.UncoreManager()
+    with pytest.raises(P.UncoreError, match="no HIP device"):
+        um.init(P.config_from_dict(CF.preset("C1")))
+
+
+@pytest.mark.parametrize("mutate,msg", [
+    (lambda s: s["system"].update(tlb_enable=1), "tlb_enable"),
+    (lambda s: s["system"].update(sys_type=1), "sys_type"),
+    (lambda s: s["system"]["cache"][0].update(share=2), "L1 share"),
+    (lambda s: s["system"]["network"].update(link_delay=0), "link_delay"),
+    (lambda s: s["system"]["directory_cache"].update(size=0), "directory"),
+    (lambda s: s["system"].update(protocol_type=1, num_levels=2,
+                                  cache=s["system"]["cache"] + [dict(s["system"]["cache"][0], share=4, level=1)]),
+     "limited-pointer"),
+])
+def test_config_validation_before_device(mutate, msg):
+    sim = CF.preset("C1")
+    mutate(sim)
+    cfg = P.config_from_dict(sim)
+    h = lib().pu_create(C.byref(cfg), 1, 0)
+    assert not h
+    assert msg in P.uncore.last_error()
+
+
+def test_stream_api_errors():
+    from primesim_amd import _abi as A
+    p = A.StreamParams(99, 16, 1, 1000, 1, 100, 1, 0, -1, 0)
+    assert lib().pu_stream_count(C.byref(p)) < 0
