@@ -107,6 +107,7 @@ def main() -> None:
     import primesim_amd as P
     from primesim_amd import _abi as A
     from primesim_amd import config as CF
+    from primesim_amd.dist import reduce_run, replica_seed
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -138,7 +139,7 @@ def main() -> None:
     streams = []
     t_gen = time.time()
     for r in range(R):
-        spec = P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=4 + 1000 * rank + r, num_quanta=64,
+        spec = P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=replica_seed(4, rank, r), num_quanta=64,
                             max_requests=per)
         s = P.generate_stream(spec)
         assert len(s) == per, (len(s), per)
@@ -191,16 +192,11 @@ def main() -> None:
     after = sum_stats(um, R)
     delta = {k: after[k] - before.get(k, 0) for k in after if k != "error_flags"}
     errf = after.get("error_flags", 0)
-    processed = R * args.chunk * args.steps
-    t_max = elapsed
-    tot_processed = processed
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_max = float(t.item())
-        n = torch.tensor([processed], dtype=torch.int64, device=dev)
-        dist.all_reduce(n, op=dist.ReduceOp.SUM)
-        tot_processed = int(n.item())
+    # requests that actually reached the uncore: a replica whose message delay
+    # went negative stops there, like the reference's handler (prime.cpp:130-134)
+    processed = int(delta["requests"])
+    halted = sum(1 for r in range(R) if um.stats(r).error_flags & A.PU_ERRF_NEG_DELAY)
+    t_max, tot_processed = reduce_run(elapsed, processed, dev)
     value = tot_processed / t_max
 
     # ---- roofline of the engine kernel (per launch, this rank)
@@ -246,7 +242,8 @@ def main() -> None:
                 "requests_per_replica_per_step": args.chunk,
                 "parallelism": f"replicas: {R} independent uncores per GPU x {world} GPU(s)",
                 "per_replica_accesses_per_s": value / (R * world),
-                "error_flags": errf,
+                "halted_replicas": halted,
+                "error_flags": errf & ~A.PU_ERRF_NEG_DELAY,
             },
             "roofline": {
                 "bound": "hbm",

@@ -215,6 +215,7 @@ struct Sys {
     std::map<std::pair<int, int>, int> core_map;
     std::vector<int64_t> completion;
     int batch_delay = 0;   // running delay of the open message, kept across cpuref_run calls
+    bool halted = false;   // prime.cpp:130-134: the handler exits on a negative delay
 
     // -------------------------------------------------- geometry
     std::string init(const pu_sim_cfg* c) {
@@ -847,6 +848,10 @@ int cpuref_alloc_core(void* h, int prog, int thread) {
 
 long cpuref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
     Sys* s = (Sys*)h;
+    if (s->halted) {
+        if (delays) std::fill_n(delays, n, 0);
+        return n ? -1 : 0;
+    }
     int delay = s->batch_delay;
     for (size_t i = 0; i < n; i++) {
         const pu_req& q = reqs[i];
@@ -859,6 +864,8 @@ long cpuref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
         if (delay < 0) {
             s->st.error_flags |= PU_ERRF_NEG_DELAY;
             s->batch_delay = delay;
+            s->halted = true;
+            if (delays) std::fill(delays + i + 1, delays + n, 0);
             return (long)i + 1;
         }
     }

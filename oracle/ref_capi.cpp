@@ -13,6 +13,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -77,6 +78,7 @@ struct RefInstance {
     ThreadSched sched;
     int num_cores = 0;
     int batch_delay = 0;   // prime.cpp's running `delay` of the open message, kept across calls
+    bool halted = false;   // prime.cpp:130-134: the handler thread exits on a negative delay
     std::vector<int64_t> completion;
 };
 
@@ -151,6 +153,10 @@ int ref_get_core_id(void* h, int prog, int thread) {
 // negative (prime.cpp:130 would kill the handler thread there).
 long ref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
     RefInstance* r = (RefInstance*)h;
+    if (r->halted) {
+        if (delays) std::fill_n(delays, n, 0);
+        return n ? -1 : 0;
+    }
     int delay = r->batch_delay;   // prime.cpp:113 `delay` is an int
     InsMem ins;
     std::memset(&ins, 0, sizeof(ins));
@@ -167,6 +173,8 @@ long ref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
         if (q.core >= 0 && q.core < r->num_cores) r->completion[(size_t)q.core] = t + d;
         if (delay < 0) {
             r->batch_delay = delay;
+            r->halted = true;
+            if (delays) std::fill(delays + i + 1, delays + n, 0);
             return (long)i + 1;
         }
     }

@@ -798,9 +798,15 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
 
     RunState* rs = e.template at<RunState>(g->off_run);
     int32_t D = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->batch_delay : 0u, 0);
+    int32_t halted = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->halted : 0u, 0);
     int64_t* completion = e.template at<int64_t>(g->off_completion);
     const uint64_t b = off[blockIdx.x], end = off[blockIdx.x + 1];
+    uint64_t done = 0;
     for (uint64_t i = b; i < end; i++) {
+        if (halted) {                       // the reference's handler thread has exited
+            if (e.ln == 0) delays[i] = 0;
+            continue;
+        }
         const pu_req q = reqs[i];
         if (q.batch_start) D = 0;
         const int64_t t = q.timer + D;
@@ -810,12 +816,17 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
             delays[i] = d;
             if (q.core >= 0 && q.core < g->num_cores) completion[q.core] = t + d;
         }
+        done++;
         D += d - 1;
-        if (D < 0) e.s_err |= PU_ERRF_NEG_DELAY;
+        if (D < 0) {                        // prime.cpp:130-134
+            e.s_err |= PU_ERRF_NEG_DELAY;
+            halted = 1;
+        }
     }
     if (e.ln == 0) {
         rs->batch_delay = D;
-        rs->processed += end - b;
+        rs->halted = halted;
+        rs->processed += done;
     }
     e.flush_stats();
 }

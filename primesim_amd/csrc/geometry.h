@@ -92,6 +92,8 @@ struct Geo {
 // Per-replica run state carried across launches.
 struct RunState {
     int32_t batch_delay;   // prime.cpp:113 running `delay` of the open message
-    int32_t _pad;
+    int32_t halted;        // 1 once a message's delay went negative: prime.cpp:130-134
+                           // prints an error and exits the handler thread, so no
+                           // further request reaches the uncore
     uint64_t processed;    // requests processed so far
 };

@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import primesim_amd as P
+from primesim_amd import _abi as A
 from golden_util import Case, assert_stats_match, case_names
 
 pytestmark = pytest.mark.gpu
@@ -25,8 +26,9 @@ def test_engine_reproduces_reference(name):
         np.testing.assert_array_equal(d, c.delays)
         np.testing.assert_array_equal(um.completion(), c.completion)
         st = um.stats().as_dict()
-        assert st["error_flags"] == 0
-        assert st["requests"] == len(c.reqs)
+        halt = c.meta.get("halt_index")
+        assert st["error_flags"] == (0 if halt is None else A.PU_ERRF_NEG_DELAY)
+        assert st["requests"] == (len(c.reqs) if halt is None else halt + 1)
         assert_stats_match(st, c)
         assert um.report() == c.report
     finally:

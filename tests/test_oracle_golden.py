@@ -11,6 +11,7 @@ import pytest
 
 import oracle as O
 import primesim_amd as P
+from primesim_amd import _abi as A
 from golden_util import Case, assert_stats_match, case_names
 
 
@@ -22,11 +23,12 @@ def test_oracle_reproduces_reference(name):
     for prog, th in c.threads:
         ref.alloc_core(prog, th)
     d, rc = ref.run(c.reqs)
-    assert rc == 0
+    halt = c.meta.get("halt_index")
+    assert rc == (0 if halt is None else halt + 1)
     np.testing.assert_array_equal(d, c.delays)
     np.testing.assert_array_equal(ref.completion(), c.completion)
     st = ref.stats().as_dict()
-    assert st["error_flags"] == 0
+    assert st["error_flags"] == (0 if halt is None else A.PU_ERRF_NEG_DELAY)
     assert_stats_match(st, c)
 
 
