@@ -129,7 +129,7 @@ def main() -> None:
     rbytes = probe.replica_bytes
     probe.close()
     free, total = torch.cuda.mem_get_info(dev)
-    R = args.replicas or max(1, min(512, int((free * 0.85) // rbytes)))
+    R = args.replicas or max(1, min(2048, int((free * 0.85) // rbytes)))
     R = max(1, R - R % 8) if R >= 8 else R
     log(f"[bench] rank {rank}: replica {rbytes / 2**20:.0f} MiB, {R} replicas, free {free / 2**30:.0f} GiB")
     um.init(cfg, replicas=R, device=local)

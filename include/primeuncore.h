@@ -171,6 +171,8 @@ typedef struct pu_stats {
 #define PU_ERRF_EMPTY_SHARER (1ull << 2)  /* *sharer_set.begin() on empty set */
 #define PU_ERRF_QUEUE        (1ull << 3)  /* queue-model precondition violated */
 #define PU_ERRF_NEG_DELAY    (1ull << 4)  /* batch delay went negative (prime.cpp:130) */
+#define PU_ERRF_POOL         (1ull << 5)  /* sharer-bitmap pool exhausted (engine limit;
+                                             raise PRIMEUNCORE_POOL_ENTRIES) */
 
 /* ------------------------------------------------------------------------
  * Engine lifetime and the hot path.

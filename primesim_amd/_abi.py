@@ -24,6 +24,7 @@ PU_ERRF_WB_MISS = 1 << 1
 PU_ERRF_EMPTY_SHARER = 1 << 2
 PU_ERRF_QUEUE = 1 << 3
 PU_ERRF_NEG_DELAY = 1 << 4
+PU_ERRF_POOL = 1 << 5
 
 
 class CacheCfg(C.Structure):

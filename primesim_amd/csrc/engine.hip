@@ -81,11 +81,25 @@ struct SetView {
     int64_t mts;
 };
 
-// One queue (link or bus) as held by the wave: uniform header + two ring
-// slots per lane (physical slots lane and lane+64).
-struct QueueView {
-    uint32_t hw;       // per lane: header dword `lane` (lanes 0..9)
+// A queue's ring as held by the wave: physical slots lane and lane+64.
+struct RingView {
     uint64_t lf, ls, hf, hs;
+};
+
+// Uniform copy of a queue header (QueueHdr dwords 0-9).
+struct QState {
+    uint32_t head, count;
+    uint64_t n;
+    double sum, sum_sq;
+    uint64_t newest;
+};
+
+// A window of up to 64 hops of one route, prefetched with lane h holding hop
+// h: its link id, its header dwords and its two front ring slots.
+struct RouteView {
+    int32_t q;
+    uint32_t d0, d1, d2, d3, d4, d5, d6, d7, d8, d9;
+    uint64_t f0, f1;     // ring[head].first, ring[head+1].first
 };
 
 template <int NL>
@@ -97,6 +111,8 @@ struct Engine {
     // reference System scratch for the requesting core (delay[core], hit_flag[core])
     int dly;
     bool hit;
+    int32_t pool_top;    // sharer-bitmap pool stack (RunState.pool_top)
+    bool stop;           // replica must stop (pool exhausted)
 
     // stats accumulated in registers, flushed once per launch
     uint64_t s_net_acc, s_net_dist, s_net_total, s_net_router, s_net_link, s_net_inject;
@@ -109,10 +125,11 @@ struct Engine {
     }
 
     // ------------------------------------------------------------ queues
-    __device__ __forceinline__ void q_issue(QueueView& v, int q) const {
-        const uint32_t* H = reinterpret_cast<const uint32_t*>(at<QueueHdr>(g->off_qhdr) + q);
-        const QueueSlot* R = at<QueueSlot>(g->off_qring) + (size_t)q * PU_QRING;
-        v.hw = ln < 10 ? H[ln] : 0u;
+    __device__ __forceinline__ QueueSlot* ring_of(int q) const {
+        return at<QueueSlot>(g->off_qring) + (size_t)q * PU_QRING;
+    }
+    __device__ __forceinline__ void ring_load(RingView& v, int q) const {
+        const QueueSlot* R = ring_of(q);
         QueueSlot a = R[ln];
         QueueSlot b = R[ln + 64];
         v.lf = a.first; v.ls = a.second;
@@ -120,14 +137,13 @@ struct Engine {
     }
 
     // M/G/1 (queue_model_m_g_1.cpp:16-42), reference operation order.
-    __device__ __forceinline__ uint64_t mg1_wait(uint64_t n, double sum, double sum_sq,
-                                                 uint64_t newest) const {
-        if (n == 0) return 0;
-        double nd = (double)n;
-        double mean = sum / nd;
-        double var = (sum_sq / nd) - mean * mean;
-        double mu = 1.0 / (sum / nd);
-        double lambda = nd / (double)newest;
+    __device__ __forceinline__ uint64_t mg1_wait(const QState& s) const {
+        if (s.n == 0) return 0;
+        double nd = (double)s.n;
+        double mean = s.sum / nd;
+        double var = (s.sum_sq / nd) - mean * mean;
+        double mu = 1.0 / (s.sum / nd);
+        double lambda = nd / (double)s.newest;
         if (lambda >= mu) lambda = 0.999 * mu;
         double inv = 1.0 / (mu * mu);
         double num = 0.5 * mu;
@@ -137,145 +153,161 @@ struct Engine {
         return (uint64_t)ceil(w);
     }
 
-    // QueueModelHistoryTree::computeQueueDelay (queue_model_history_tree.cpp:42-125)
-    // on the ring view; writes the queue back.  Returns the queue delay.
-    __device__ uint64_t q_apply(QueueView& v, int q, uint64_t t, uint64_t p, uint64_t minp) {
-        uint32_t head = rl32(v.hw, 0), cnt = rl32(v.hw, 1);
-        uint64_t n = ((uint64_t)rl32(v.hw, 3) << 32) | rl32(v.hw, 2);
-        double sum = __longlong_as_double((long long)(((uint64_t)rl32(v.hw, 5) << 32) | rl32(v.hw, 4)));
-        double sum_sq = __longlong_as_double((long long)(((uint64_t)rl32(v.hw, 7) << 32) | rl32(v.hw, 6)));
-        uint64_t newest = ((uint64_t)rl32(v.hw, 9) << 32) | rl32(v.hw, 8);
-
-        if (cnt >= PU_QMAX) {           // prune the minimum (history_tree.cpp:49-55)
-            head = (head + 1) & (PU_QRING - 1);
-            cnt--;
-        }
+    // Tree branch of QueueModelHistoryTree::computeQueueDelay
+    // (queue_model_history_tree.cpp:64-112) on the full ring.  head/cnt are the
+    // post-prune values and are updated; edited slots are written back.
+    __device__ uint64_t tree_op(int q, const RingView& v, uint32_t& head, uint32_t& cnt, uint64_t t, uint64_t p,
+                                uint64_t minp) {
         const uint64_t tp = t + p;
-        uint64_t front_first = head < 64 ? rl64(v.lf, (int)head) : rl64(v.hf, (int)(head - 64));
-        uint64_t d;
-        // pending ring edits
-        int op = 0;  // 0 none, 1 second<-t, 2 first<-x, 3 remove, 4 split
-        uint32_t k = 0;
-        uint64_t nf = 0, node_second = 0;
-        if (front_first > tp) {        // analytical model (history_tree.cpp:58-63)
-            d = mg1_wait(n, sum, sum_sq, newest);
-            s_mg1++;
+        const uint32_t jl = ((uint32_t)ln - head) & (PU_QRING - 1);
+        const uint32_t jh = ((uint32_t)ln + 64 - head) & (PU_QRING - 1);
+        bool pl = jl < cnt && ((v.lf <= t && tp <= v.ls) || (t < v.lf && v.ls - v.lf >= p));
+        bool ph = jh < cnt && ((v.hf <= t && tp <= v.hs) || (t < v.hf && v.hs - v.hf >= p));
+        uint64_t ml = ballot(pl), mh = ballot(ph);
+        // leftmost interval in logical (ring) order starting at `head`
+        uint32_t slot;
+        if (head < 64) {
+            uint64_t ge = ml & (~0ull << head);
+            if (ge) slot = (uint32_t)__builtin_ctzll(ge);
+            else if (mh) slot = 64 + (uint32_t)__builtin_ctzll(mh);
+            else slot = (uint32_t)__builtin_ctzll(ml);
         } else {
-            const uint32_t jl = ((uint32_t)ln - head) & (PU_QRING - 1);
-            const uint32_t jh = ((uint32_t)ln + 64 - head) & (PU_QRING - 1);
-            bool pl = jl < cnt && ((v.lf <= t && tp <= v.ls) || (t < v.lf && v.ls - v.lf >= p));
-            bool ph = jh < cnt && ((v.hf <= t && tp <= v.hs) || (t < v.hf && v.hs - v.hf >= p));
-            uint64_t ml = ballot(pl), mh = ballot(ph);
-            // leftmost in logical (ring) order starting at `head`
-            uint32_t slot;
-            if (head < 64) {
-                uint64_t ge = ml & (~0ull << head);
-                if (ge) slot = (uint32_t)__builtin_ctzll(ge);
-                else if (mh) slot = 64 + (uint32_t)__builtin_ctzll(mh);
-                else slot = (uint32_t)__builtin_ctzll(ml);
+            uint64_t ge = mh & (~0ull << (head - 64));
+            if (ge) slot = 64 + (uint32_t)__builtin_ctzll(ge);
+            else if (ml) slot = (uint32_t)__builtin_ctzll(ml);
+            else slot = 64 + (uint32_t)__builtin_ctzll(mh);
+        }
+        if ((ml | mh) == 0) {      // search returned NULL: an assert in the reference
+            s_err |= PU_ERRF_QUEUE;
+            slot = head;
+        }
+        const uint32_t k = (slot - head) & (PU_QRING - 1);
+        const uint64_t f = slot < 64 ? rl64(v.lf, (int)slot) : rl64(v.hf, (int)(slot - 64));
+        const uint64_t s = slot < 64 ? rl64(v.ls, (int)slot) : rl64(v.hs, (int)(slot - 64));
+        uint64_t d;
+        int op;  // 1 second<-t, 2 first<-nf, 3 remove, 4 split
+        uint64_t nf = 0;
+        if (t >= f) {
+            d = 0;
+            if (t - f >= minp) {
+                op = (s - tp >= minp) ? 4 : 1;
+            } else if (s - tp >= minp) {
+                op = 2;
+                nf = tp;
             } else {
-                uint64_t ge = mh & (~0ull << (head - 64));
-                if (ge) slot = 64 + (uint32_t)__builtin_ctzll(ge);
-                else if (ml) slot = (uint32_t)__builtin_ctzll(ml);
-                else slot = 64 + (uint32_t)__builtin_ctzll(mh);
+                op = 3;
             }
-            if ((ml | mh) == 0) {      // tree search returned NULL: assert in the reference
-                s_err |= PU_ERRF_QUEUE;
-                slot = head;
-            }
-            k = (slot - head) & (PU_QRING - 1);
-            uint64_t f = slot < 64 ? rl64(v.lf, (int)slot) : rl64(v.hf, (int)(slot - 64));
-            uint64_t s = slot < 64 ? rl64(v.ls, (int)slot) : rl64(v.hs, (int)(slot - 64));
-            node_second = s;
-            if (t >= f) {
-                d = 0;
-                if (t - f >= minp) {
-                    op = (s - tp >= minp) ? 4 : 1;
-                } else if (s - tp >= minp) {
-                    op = 2;
-                    nf = tp;
-                } else {
-                    op = 3;
-                }
+        } else {
+            d = f - t;
+            if (s - (f + p) >= minp) {
+                op = 2;
+                nf = f + p;
             } else {
-                d = f - t;
-                if (s - (f + p) >= minp) {
-                    op = 2;
-                    nf = f + p;
-                } else {
-                    op = 3;
-                }
+                op = 3;
             }
         }
-
-        // ---- apply ring edit (logical positions relative to `head`)
-        uint32_t new_head = head, new_cnt = cnt;
         bool dl = false, dh = false;
         uint64_t lf = v.lf, ls = v.ls, hf = v.hf, hs = v.hs;
-        if (op != 0) {
-            const uint32_t jl = ((uint32_t)ln - head) & (PU_QRING - 1);
-            const uint32_t jh = ((uint32_t)ln + 64 - head) & (PU_QRING - 1);
-            if (op == 1 || op == 2) {
-                if (jl == k) { if (op == 1) ls = t; else lf = nf; dl = true; }
-                if (jh == k) { if (op == 1) hs = t; else hf = nf; dh = true; }
-            } else if (op == 3) {
-                if (k == 0) {
-                    new_head = (head + 1) & (PU_QRING - 1);
-                } else {
-                    // logical [k+1, cnt) move down by one: slot s takes slot s+1
-                    const int src = (ln + 1) & 63;
-                    uint64_t a_f = shfl64(v.lf, src), a_s = shfl64(v.ls, src);
-                    uint64_t b_f = shfl64(v.hf, src), b_s = shfl64(v.hs, src);
-                    uint64_t sl_f = ln == 63 ? b_f : a_f, sl_s = ln == 63 ? b_s : a_s;
-                    uint64_t sh_f = ln == 63 ? a_f : b_f, sh_s = ln == 63 ? a_s : b_s;
-                    if (jl >= k && jl + 1 < cnt) { lf = sl_f; ls = sl_s; dl = true; }
-                    if (jh >= k && jh + 1 < cnt) { hf = sh_f; hs = sh_s; dh = true; }
-                }
-                new_cnt = cnt - 1;
-            } else {  // split: node k keeps [first, t], [t+p, second] inserted at k+1
-                const int src = (ln + 63) & 63;
+        if (op == 1 || op == 2) {
+            if (jl == k) { if (op == 1) ls = t; else lf = nf; dl = true; }
+            if (jh == k) { if (op == 1) hs = t; else hf = nf; dh = true; }
+        } else if (op == 3) {
+            if (k == 0) {
+                head = (head + 1) & (PU_QRING - 1);
+            } else {
+                // logical [k+1, cnt) move down one: slot s takes slot s+1
+                const int src = (ln + 1) & 63;
                 uint64_t a_f = shfl64(v.lf, src), a_s = shfl64(v.ls, src);
                 uint64_t b_f = shfl64(v.hf, src), b_s = shfl64(v.hs, src);
-                uint64_t pl_f = ln == 0 ? b_f : a_f, pl_s = ln == 0 ? b_s : a_s;
-                uint64_t ph_f = ln == 0 ? a_f : b_f, ph_s = ln == 0 ? a_s : b_s;
-                if (jl == k) { ls = t; dl = true; }
-                else if (jl == k + 1) { lf = tp; ls = node_second; dl = true; }
-                else if (jl >= k + 2 && jl <= cnt) { lf = pl_f; ls = pl_s; dl = true; }
-                if (jh == k) { hs = t; dh = true; }
-                else if (jh == k + 1) { hf = tp; hs = node_second; dh = true; }
-                else if (jh >= k + 2 && jh <= cnt) { hf = ph_f; hs = ph_s; dh = true; }
-                new_cnt = cnt + 1;
+                uint64_t sl_f = ln == 63 ? b_f : a_f, sl_s = ln == 63 ? b_s : a_s;
+                uint64_t sh_f = ln == 63 ? a_f : b_f, sh_s = ln == 63 ? a_s : b_s;
+                if (jl >= k && jl + 1 < cnt) { lf = sl_f; ls = sl_s; dl = true; }
+                if (jh >= k && jh + 1 < cnt) { hf = sh_f; hs = sh_s; dh = true; }
             }
+            cnt = cnt - 1;
+        } else {  // split: node k keeps [first, t]; [t+p, second] inserted at k+1
+            const int src = (ln + 63) & 63;
+            uint64_t a_f = shfl64(v.lf, src), a_s = shfl64(v.ls, src);
+            uint64_t b_f = shfl64(v.hf, src), b_s = shfl64(v.hs, src);
+            uint64_t pl_f = ln == 0 ? b_f : a_f, pl_s = ln == 0 ? b_s : a_s;
+            uint64_t ph_f = ln == 0 ? a_f : b_f, ph_s = ln == 0 ? a_s : b_s;
+            if (jl == k) { ls = t; dl = true; }
+            else if (jl == k + 1) { lf = tp; ls = s; dl = true; }
+            else if (jl >= k + 2 && jl <= cnt) { lf = pl_f; ls = pl_s; dl = true; }
+            if (jh == k) { hs = t; dh = true; }
+            else if (jh == k + 1) { hf = tp; hs = s; dh = true; }
+            else if (jh >= k + 2 && jh <= cnt) { hf = ph_f; hs = ph_s; dh = true; }
+            cnt = cnt + 1;
         }
-        // ---- M/G/1 update (queue_model_m_g_1.cpp:45-55) — always
-        sum_sq = sum_sq + (double)p * (double)p;
-        sum = sum + (double)p;
-        n = n + 1;
-        uint64_t fin = t + d + p;
-        newest = fin > newest ? fin : newest;
-
-        // ---- write back (owners only)
-        QueueSlot* R = at<QueueSlot>(g->off_qring) + (size_t)q * PU_QRING;
+        QueueSlot* R = ring_of(q);
         if (dl) R[ln] = QueueSlot{lf, ls};
         if (dh) R[ln + 64] = QueueSlot{hf, hs};
+        return d;
+    }
+
+    // M/G/1 update (queue_model_m_g_1.cpp:45-55) and header write-back.
+    __device__ __forceinline__ void q_finish(int q, QState& st, uint64_t t, uint64_t p, uint64_t d) {
+        st.sum_sq = st.sum_sq + (double)p * (double)p;
+        st.sum = st.sum + (double)p;
+        st.n = st.n + 1;
+        uint64_t fin = t + d + p;
+        st.newest = fin > st.newest ? fin : st.newest;
         if (ln < 10) {
-            uint64_t sb = (uint64_t)__double_as_longlong(sum), qb = (uint64_t)__double_as_longlong(sum_sq);
+            uint64_t sb = (uint64_t)__double_as_longlong(st.sum), qb = (uint64_t)__double_as_longlong(st.sum_sq);
             uint32_t w;
             switch (ln) {
-                case 0: w = new_head; break;
-                case 1: w = new_cnt; break;
-                case 2: w = (uint32_t)n; break;
-                case 3: w = (uint32_t)(n >> 32); break;
+                case 0: w = st.head; break;
+                case 1: w = st.count; break;
+                case 2: w = (uint32_t)st.n; break;
+                case 3: w = (uint32_t)(st.n >> 32); break;
                 case 4: w = (uint32_t)sb; break;
                 case 5: w = (uint32_t)(sb >> 32); break;
                 case 6: w = (uint32_t)qb; break;
                 case 7: w = (uint32_t)(qb >> 32); break;
-                case 8: w = (uint32_t)newest; break;
-                default: w = (uint32_t)(newest >> 32); break;
+                case 8: w = (uint32_t)st.newest; break;
+                default: w = (uint32_t)(st.newest >> 32); break;
             }
             reinterpret_cast<uint32_t*>(at<QueueHdr>(g->off_qhdr) + q)[ln] = w;
         }
+    }
+
+    // One computeQueueDelay given the header and the first two interval starts.
+    __device__ __forceinline__ uint64_t q_step(int q, QState& st, uint64_t f0, uint64_t f1, uint64_t t, uint64_t p,
+                                               uint64_t minp) {
+        uint64_t front = f0;
+        if (st.count >= PU_QMAX) {      // prune the minimum (history_tree.cpp:49-55)
+            st.head = (st.head + 1) & (PU_QRING - 1);
+            st.count--;
+            front = f1;
+        }
+        uint64_t d;
+        if (front > t + p) {             // older than the tracked history: M/G/1 (history_tree.cpp:58-63)
+            d = mg1_wait(st);
+            s_mg1++;
+        } else {
+            RingView v;
+            ring_load(v, q);
+            d = tree_op(q, v, st.head, st.count, t, p, minp);
+        }
+        q_finish(q, st, t, p, d);
         return d;
+    }
+
+    // A whole queue op loading its own state (bus queues, unit tests).
+    __device__ uint64_t q_op(int q, uint64_t t, uint64_t p, uint64_t minp) {
+        const uint32_t* H = reinterpret_cast<const uint32_t*>(at<QueueHdr>(g->off_qhdr) + q);
+        uint32_t hw = ln < 10 ? H[ln] : 0u;
+        QState st;
+        st.head = rl32(hw, 0);
+        st.count = rl32(hw, 1);
+        st.n = ((uint64_t)rl32(hw, 3) << 32) | rl32(hw, 2);
+        st.sum = __longlong_as_double((long long)(((uint64_t)rl32(hw, 5) << 32) | rl32(hw, 4)));
+        st.sum_sq = __longlong_as_double((long long)(((uint64_t)rl32(hw, 7) << 32) | rl32(hw, 6)));
+        st.newest = ((uint64_t)rl32(hw, 9) << 32) | rl32(hw, 8);
+        const QueueSlot* R = ring_of(q);
+        uint32_t h0 = st.head, h1 = (st.head + 1) & (PU_QRING - 1);
+        uint64_t f0 = R[h0].first, f1 = R[h1].first;
+        return q_step(q, st, uni64(f0), uni64(f1), t, p, minp);
     }
 
     // ------------------------------------------------------------ network
@@ -332,6 +364,30 @@ struct Engine {
         return link_of(rx, ry, z, u ? 4 : 5);
     }
 
+    // Prefetch hops [b0, b0+64) of a route: lane h loads hop b0+h's link
+    // header and the two interval starts at its ring head (two dependent
+    // loads per lane, all hops in flight together).
+    __device__ __forceinline__ void route_load(RouteView& rv, int b0, int hops, int sx, int sy, int sz, int rx,
+                                               int ry, int rz, int hx, int hy) const {
+        const int h = b0 + ln;
+        rv.q = 0;
+        rv.d0 = rv.d1 = rv.d2 = rv.d3 = rv.d4 = rv.d5 = rv.d6 = rv.d7 = rv.d8 = rv.d9 = 0;
+        rv.f0 = rv.f1 = 0;
+        if (h < hops) {
+            const int q = route_link(h, sx, sy, sz, rx, ry, rz, hx, hy);
+            rv.q = q;
+            const uint4* H = reinterpret_cast<const uint4*>(at<QueueHdr>(g->off_qhdr) + q);
+            uint4 a = H[0], b = H[1];
+            uint2 c = reinterpret_cast<const uint2*>(H + 2)[0];
+            rv.d0 = a.x; rv.d1 = a.y; rv.d2 = a.z; rv.d3 = a.w;
+            rv.d4 = b.x; rv.d5 = b.y; rv.d6 = b.z; rv.d7 = b.w;
+            rv.d8 = c.x; rv.d9 = c.y;
+            const QueueSlot* R = ring_of(q);
+            rv.f0 = R[a.x].first;
+            rv.f1 = R[(a.x + 1) & (PU_QRING - 1)].first;
+        }
+    }
+
     // Network::transmit (network.cpp:97-160)
     __device__ uint64_t transmit(int src, int dst, int len, uint64_t timer) {
         if (src == dst) return 0;
@@ -343,20 +399,23 @@ struct Engine {
         const int hops = hx + hy + hz;
         const uint64_t router = g->router_delay, link_delay = g->link_delay;
         uint64_t t = timer + g->inject_delay;
-        QueueView cur, nxt;
-        int qc = route_link(0, sx, sy, sz, rx, ry, rz, hx, hy);
-        q_issue(cur, qc);
-        for (int h = 0; h < hops; h++) {
-            int qn = 0;
-            if (h + 1 < hops) {
-                qn = route_link(h + 1, sx, sy, sz, rx, ry, rz, hx, hy);
-                q_issue(nxt, qn);
+        for (int b0 = 0; b0 < hops; b0 += 64) {
+            RouteView rv;
+            route_load(rv, b0, hops, sx, sy, sz, rx, ry, rz, hx, hy);
+            const int nh = hops - b0 < 64 ? hops - b0 : 64;
+            for (int j = 0; j < nh; j++) {
+                t += router;
+                const int q = (int)rl32((uint32_t)rv.q, j);
+                QState st;
+                st.head = rl32(rv.d0, j);
+                st.count = rl32(rv.d1, j);
+                st.n = ((uint64_t)rl32(rv.d3, j) << 32) | rl32(rv.d2, j);
+                st.sum = __longlong_as_double((long long)(((uint64_t)rl32(rv.d5, j) << 32) | rl32(rv.d4, j)));
+                st.sum_sq = __longlong_as_double((long long)(((uint64_t)rl32(rv.d7, j) << 32) | rl32(rv.d6, j)));
+                st.newest = ((uint64_t)rl32(rv.d9, j) << 32) | rl32(rv.d8, j);
+                t += q_step(q, st, rl64(rv.f0, j), rl64(rv.f1, j), t, (uint64_t)plen, link_delay) + link_delay;
+                s_flits += (uint64_t)plen;
             }
-            t += router;
-            t += q_apply(cur, qc, t, (uint64_t)plen, link_delay) + link_delay;
-            s_flits += (uint64_t)plen;
-            cur = nxt;
-            qc = qn;
         }
         t += router;
         t += (uint64_t)(plen - 1);
@@ -498,47 +557,124 @@ struct Engine {
         }
     }
 
-    // ------------------------------------------------------------ sharer bitmaps
-    __device__ __forceinline__ int first_sharer(uint64_t sw, int nw) {
-        uint64_t m = ballot(ln < nw && sw != 0);
-        if (!m) {
-            s_err |= PU_ERRF_EMPTY_SHARER;
-            return 0;
-        }
-        int k = (int)__builtin_ctzll(m);
-        return k * 64 + (int)__builtin_ctzll(rl64(sw, k));
+    // ------------------------------------------------------------ sharer sets
+    // Line::sharer_set (a std::set<int>, cache.h:86): up to 4 ids inline in
+    // `sh`, ascending, 16 bits each; a fifth sharer moves the set to a full-map
+    // bitmap from the replica's pool (lane k holds word k).
+    __device__ __forceinline__ uint64_t* pool_of(uint64_t idx) const {
+        return at<uint64_t>(g->dir.off_pool) + idx * (uint64_t)g->dir.nwords;
     }
-    __device__ __forceinline__ int count_sharers(uint64_t sw, int nw) const {
-        int c = ln < nw ? __builtin_popcountll(sw) : 0;
+    __device__ __forceinline__ uint64_t pool_word(uint64_t idx) const {
+        return ln < g->dir.nwords ? pool_of(idx)[ln] : 0ull;
+    }
+    __device__ __forceinline__ void pool_release(uint32_t nsh, uint64_t sh) {
+        if (nsh != PU_SH_POOL) return;
+        if (ln == 0) at<int32_t>(g->dir.off_pool_free)[pool_top] = (int32_t)sh;
+        pool_top++;
+    }
+    __device__ __forceinline__ bool pool_alloc(uint64_t* idx) {
+        if (pool_top <= 0) {
+            s_err |= PU_ERRF_POOL;
+            stop = true;
+            return false;
+        }
+        pool_top--;
+        uint32_t v = ln == 0 ? (uint32_t)at<int32_t>(g->dir.off_pool_free)[pool_top] : 0u;
+        *idx = rl32(v, 0);
+        return true;
+    }
+    __device__ int first_sharer(uint32_t nsh, uint64_t sh) {
+        if (nsh == PU_SH_POOL) {
+            uint64_t w = pool_word(sh);
+            uint64_t m = ballot(w != 0);
+            if (m) {
+                int k = (int)__builtin_ctzll(m);
+                return k * 64 + (int)__builtin_ctzll(rl64(w, k));
+            }
+        } else if (nsh > 0) {
+            return (int)(sh & 0xFFFF);
+        }
+        s_err |= PU_ERRF_EMPTY_SHARER;     // *sharer_set.begin() on an empty set
+        return 0;
+    }
+    __device__ int count_sharers(uint32_t nsh, uint64_t sh) const {
+        if (nsh != PU_SH_POOL) return (int)nsh;
+        int c = __builtin_popcountll(pool_word(sh));
         for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
         return (int)uni32((uint32_t)c);
+    }
+    // sharer_set.insert(cid)
+    __device__ void add_sharer(uint32_t& nsh, uint64_t& sh, int cid) {
+        if (nsh == PU_SH_POOL) {
+            if (ln == (cid >> 6)) {
+                uint64_t* P = pool_of(sh);
+                P[ln] = P[ln] | (1ull << (cid & 63));
+            }
+            return;
+        }
+        int below = 0;
+        bool present = false;
+        for (uint32_t i = 0; i < nsh; i++) {
+            int id = (int)((sh >> (16 * i)) & 0xFFFF);
+            present |= id == cid;
+            below += id < cid;
+        }
+        if (present) return;
+        if (nsh < PU_SH_INLINE) {
+            uint64_t low = below == 0 ? 0ull : ((1ull << (16 * below)) - 1);
+            sh = (sh & low) | ((uint64_t)cid << (16 * below)) | ((sh & ~low) << 16);
+            nsh++;
+            return;
+        }
+        uint64_t idx;
+        if (!pool_alloc(&idx)) return;
+        uint64_t w = 0;
+        for (int i = 0; i < PU_SH_INLINE; i++) {
+            int id = (int)((sh >> (16 * i)) & 0xFFFF);
+            if ((id >> 6) == ln) w |= 1ull << (id & 63);
+        }
+        if ((cid >> 6) == ln) w |= 1ull << (cid & 63);
+        if (ln < g->dir.nwords) pool_of(idx)[ln] = w;
+        nsh = PU_SH_POOL;
+        sh = idx;
     }
 
     // home -> sharer -> inval -> home for every sharer in ascending id
     // (system.cpp:605-618, 660-671, 766-779, 820-831)
-    __device__ int inval_sharers(uint64_t sw, int nw, int home, const Req& r, int64_t base_t) {
-        const int last = NL - 1;
+    __device__ int inval_sharers(uint32_t nsh, uint64_t sh, int home, const Req& r, int64_t base_t) {
+        constexpr int last = NL - 1;
         int pipe = 0, mx = 0;
-        uint64_t rem = ln < nw ? sw : 0;
-        while (true) {
-            uint64_t m = ballot(rem != 0);
-            if (!m) break;
-            int k = (int)__builtin_ctzll(m);
-            uint64_t word = rl64(rem, k);
-            int p = k * 64 + (int)__builtin_ctzll(word);
-            if (ln == k) rem &= rem - 1;
-            int t = pipe;
-            t += (int)transmit(home, p, 0, (uint64_t)(base_t + t));
-            t += down<last, true>(p, r);
-            t += (int)transmit(p, home, 0, (uint64_t)(base_t + t));
-            mx = t > mx ? t : mx;
-            pipe += g->header_flits;
+        if (nsh == PU_SH_POOL) {
+            uint64_t rem = pool_word(sh);
+            while (true) {
+                uint64_t m = ballot(rem != 0);
+                if (!m) break;
+                int k = (int)__builtin_ctzll(m);
+                int p = k * 64 + (int)__builtin_ctzll(rl64(rem, k));
+                if (ln == k) rem &= rem - 1;
+                int t = pipe;
+                t += (int)transmit(home, p, 0, (uint64_t)(base_t + t));
+                t += down<last, true>(p, r);
+                t += (int)transmit(p, home, 0, (uint64_t)(base_t + t));
+                mx = t > mx ? t : mx;
+                pipe += g->header_flits;
+            }
+        } else {
+            for (uint32_t i = 0; i < nsh; i++) {
+                int p = (int)((sh >> (16 * i)) & 0xFFFF);
+                int t = pipe;
+                t += (int)transmit(home, p, 0, (uint64_t)(base_t + t));
+                t += down<last, true>(p, r);
+                t += (int)transmit(p, home, 0, (uint64_t)(base_t + t));
+                mx = t > mx ? t : mx;
+                pipe += g->header_flits;
+            }
         }
         return mx;
     }
     // broadcast to every core (system.cpp:621-633 etc.; N == num_cores enforced)
     __device__ int broadcast(int home, const Req& r, int64_t base_t) {
-        const int last = NL - 1;
+        constexpr int last = NL - 1;
         int pipe = 0, mx = 0;
         s_bcast++;
         for (int i = 0; i < g->num_cores; i++) {
@@ -553,99 +689,141 @@ struct Engine {
     }
 
     // ------------------------------------------------------------ home slice
-    // accessSharedCache (system.cpp:734-893) / accessDirectoryCache (577-731)
+    // accessSharedCache (system.cpp:734-893) / accessDirectoryCache (577-731).
+    // The home line is read once (lane w: way w, 32 B) and written once at the
+    // end: nothing reached from here touches directory lines.
     __device__ int access_home(int cid, int home, const Req& r, int64_t timer, uint32_t* out_state) {
         const DirGeo& D = g->dir;
         const bool shared = g->shared_llc != 0;
-        const int last = NL - 1;
+        constexpr int last = NL - 1;
         const int blk = (int)g->lv[last].block;
-        const int nw = D.nwords;
-        LineMeta* meta = at<LineMeta>(D.off_meta);
-        int64_t* tsa = at<int64_t>(D.off_ts);
-        uint64_t* sh = at<uint64_t>(D.off_sh);
+        DirLine* lines = at<DirLine>(D.off_line);
         if (ln == (home & 63)) at<uint32_t>(D.off_alive)[home] = 1u;   // home_stat[home] = 1
-        SetView v;
-        set_load(v, meta, tsa, D.nsets, D.nways, D.offbits, D.idxbits, (uint64_t)home, r.addr);
-        int way = set_find(v, D.nways, r.prog);
+        const uint64_t set = (r.addr >> D.offbits) % D.nsets;
+        const uint64_t tag = r.addr >> (D.offbits + D.idxbits);
+        const uint64_t line0 = ((uint64_t)home * D.nsets + set) * D.nways;
+        const bool mine = (uint64_t)ln < D.nways;
+        DirLine m;
+        if (mine) {
+            m = lines[line0 + (uint64_t)ln];
+        } else {
+            m.tag = 0; m.id = 0; m.state = ST_I; m.nsh = 0; m._pad = 0; m.sh = 0; m.ts = INT64_MAX;
+        }
+        const uint64_t hm = ballot(mine && m.state != ST_I && m.id == r.prog && m.tag == tag);
+        int way = hm ? (int)__builtin_ctzll(hm) : -1;
         count(D.off_cnt, home, 0);
         int delay = D.access_time;
-        uint32_t st;
+        uint32_t st, nsh;
+        uint64_t sh;
         if (way < 0 && r.type != PU_WB) {
-            uint32_t old_st;
-            uint64_t old_addr;
-            int old_prog;
-            way = set_replace(v, meta, D.nways, D.offbits, D.idxbits, r.prog, &old_st, &old_addr, &old_prog);
-            uint64_t* lsh = sh + (v.line0 + (uint64_t)way) * (uint64_t)nw;
-            uint64_t sw = ln < nw ? lsh[ln] : 0;
+            // replaceLine (cache.cpp:204-235): first invalid way, else LRU
+            const uint64_t inv = ballot(mine && m.state == ST_I);
+            uint32_t old_st = ST_I;
+            uint64_t old_addr = 0;
+            int old_prog = 0;
+            if (inv) {
+                way = (int)__builtin_ctzll(inv);
+            } else {
+                int64_t bt = m.ts;
+                int bw = mine ? ln : 64;
+                for (int o = 32; o >= 1; o >>= 1) {
+                    int64_t ot = (int64_t)shfl64((uint64_t)bt, ln ^ o);
+                    int ow = __shfl(bw, ln ^ o, 64);
+                    if (ot < bt || (ot == bt && ow < bw)) {
+                        bt = ot;
+                        bw = ow;
+                    }
+                }
+                way = (int)uni32((uint32_t)bw);
+                old_st = rl32(m.state, way);
+                old_addr = (set << D.offbits) | (rl64(m.tag, way) << (D.offbits + D.idxbits));
+                old_prog = (int)rl32((uint32_t)m.id, way);
+            }
+            nsh = rl32(m.nsh, way);
+            sh = rl64(m.sh, way);
             if (old_st != ST_I) {
                 count(D.off_cnt, home, 2);
                 Req o{old_addr, old_prog, PU_RD};
                 if (old_st == ST_M || old_st == ST_E) {
-                    int own = first_sharer(sw, nw);
+                    int own = first_sharer(nsh, sh);
                     delay += (int)transmit(home, own, 0, (uint64_t)(timer + delay));
                     delay += down<last, true>(own, o);
                     int reply = (!shared || old_st == ST_M) ? blk : 0;
                     delay += (int)transmit(own, home, reply, (uint64_t)(timer + delay));
                     dram();
                 } else if (old_st == ST_S) {
-                    delay += inval_sharers(sw, nw, home, o, timer + delay);
+                    delay += inval_sharers(nsh, sh, home, o, timer + delay);
                 } else if (old_st == ST_B) {
                     delay += broadcast(home, o, timer + delay);
                 }
             }
             st = r.type == PU_WR ? ST_M : ST_E;
-            set_state(v, meta, way, st);
             count(D.off_cnt, home, 1);
-            if (ln < nw) lsh[ln] = (ln == (cid >> 6)) ? (1ull << (cid & 63)) : 0ull;
+            pool_release(nsh, sh);            // sharer_set.clear(); insert(cache_id)
+            nsh = 1;
+            sh = (uint64_t)cid;
             delay += dram();
         } else if (way < 0) {
-            s_err |= PU_ERRF_WB_MISS;     // WB missed at home: NULL deref in the reference (Q13)
+            s_err |= PU_ERRF_WB_MISS;         // WB missed at home: NULL deref in the reference (Q13)
             *out_state = ST_I;
             return delay;
         } else {
-            st = rl32(v.mst, way);
-            uint64_t* lsh = sh + (v.line0 + (uint64_t)way) * (uint64_t)nw;
-            uint64_t sw = ln < nw ? lsh[ln] : 0;
+            st = rl32(m.state, way);
+            nsh = rl32(m.nsh, way);
+            sh = rl64(m.sh, way);
             if (r.type == PU_WR) {
                 if (st == ST_M || st == ST_E) {
-                    int own = first_sharer(sw, nw);
+                    int own = first_sharer(nsh, sh);
                     delay += (int)transmit(home, own, 0, (uint64_t)(timer + delay));
                     delay += down<last, true>(own, r);
                     delay += (int)transmit(own, home, blk, (uint64_t)(timer + delay));
                 } else if (st == ST_S) {
-                    delay += inval_sharers(sw, nw, home, r, timer + delay);
+                    delay += inval_sharers(nsh, sh, home, r, timer + delay);
                     if (!shared) delay += dram();
                 } else if (st == ST_B) {
                     delay += broadcast(home, r, timer + delay);
                     if (!shared) delay += dram();
                 }
                 st = ST_M;
-                if (ln < nw) lsh[ln] = (ln == (cid >> 6)) ? (1ull << (cid & 63)) : 0ull;
+                pool_release(nsh, sh);
+                nsh = 1;
+                sh = (uint64_t)cid;
             } else if (r.type == PU_RD) {
                 if (st == ST_M || st == ST_E) {
-                    int own = first_sharer(sw, nw);
+                    int own = first_sharer(nsh, sh);
                     delay += (int)transmit(home, own, 0, (uint64_t)(timer + delay));
                     delay += down<last, false>(own, r);
                     delay += (int)transmit(own, home, blk, (uint64_t)(timer + delay));
                     st = ST_S;
                 } else if (st == ST_S) {
                     if (!shared) delay += dram();
-                    if (g->protocol_type == 1 && count_sharers(sw, nw) >= g->max_num_sharers) st = ST_B;
+                    if (g->protocol_type == 1 && count_sharers(nsh, sh) >= g->max_num_sharers) st = ST_B;
                 } else if (st == ST_B) {
                     if (!shared) delay += dram();
                 } else if (st == ST_V) {
                     st = ST_E;
                 }
-                if (ln == (cid >> 6)) lsh[ln] = sw | (1ull << (cid & 63));
+                add_sharer(nsh, sh, cid);
             } else {
                 st = shared ? ST_V : ST_I;
-                if (ln < nw) lsh[ln] = 0ull;
+                pool_release(nsh, sh);
+                nsh = 0;
+                sh = 0;
                 dram();
             }
-            set_state(v, meta, way, st);
         }
         *out_state = st == ST_B ? ST_S : st;
-        set_ts(v, tsa, way, timer);
+        if (ln == way) {
+            DirLine nl;
+            nl.tag = tag;
+            nl.id = r.prog;
+            nl.state = (uint8_t)st;
+            nl.nsh = (uint8_t)nsh;
+            nl._pad = 0;
+            nl.sh = sh;
+            nl.ts = timer;                    // home slices stamp the arrival time (Q4)
+            lines[line0 + (uint64_t)way] = nl;
+        }
         return delay;
     }
 
@@ -668,12 +846,9 @@ struct Engine {
         set_load(v, meta, tsa, L.nsets, L.nways, L.offbits, L.idxbits, (uint64_t)cid, r.addr);
         mark_alive(LV, cid);
         if (L.has_bus) {              // Bus::access (bus.cpp:55-61)
-            QueueView bq;
-            int q = L.bus_q0 + cid;
-            q_issue(bq, q);
             s_busacc++;
             uint64_t bl = (uint64_t)g->bus_latency;
-            int db = (int)q_apply(bq, q, (uint64_t)(timer + dly), bl, bl);
+            int db = (int)q_op(L.bus_q0 + cid, (uint64_t)(timer + dly), bl, bl);
             s_bus_cont += (uint64_t)(int64_t)db;
             dly += db;
         }
@@ -799,6 +974,8 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
     RunState* rs = e.template at<RunState>(g->off_run);
     int32_t D = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->batch_delay : 0u, 0);
     int32_t halted = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->halted : 0u, 0);
+    e.pool_top = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->pool_top : 0u, 0);
+    e.stop = false;
     int64_t* completion = e.template at<int64_t>(g->off_completion);
     const uint64_t b = off[blockIdx.x], end = off[blockIdx.x + 1];
     uint64_t done = 0;
@@ -822,11 +999,13 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
             e.s_err |= PU_ERRF_NEG_DELAY;
             halted = 1;
         }
+        if (e.stop) halted = 1;            // engine limit hit (sharer pool): cannot continue exactly
     }
     if (e.ln == 0) {
         rs->batch_delay = D;
         rs->halted = halted;
         rs->processed += done;
+        rs->pool_top = e.pool_top;
     }
     e.flush_stats();
 }
@@ -862,10 +1041,10 @@ __global__ __launch_bounds__(64) void unit_queue_kernel(const Geo* __restrict__ 
     e.base = base;
     e.s_mg1 = 0;
     e.s_err = 0;
+    e.pool_top = 0;
+    e.stop = false;
     for (uint64_t i = 0; i < n; i++) {
-        QueueView v;
-        e.q_issue(v, 0);
-        uint64_t d = e.q_apply(v, 0, t[i], p[i], minp);
+        uint64_t d = e.q_op(0, t[i], p[i], minp);
         if (e.ln == 0) out[i] = d;
     }
     if (e.ln == 0) *mg1 = e.s_mg1;
@@ -884,6 +1063,8 @@ __global__ __launch_bounds__(64) void unit_network_kernel(const Geo* __restrict_
     e.s_net_acc = e.s_net_dist = e.s_net_total = e.s_net_router = e.s_net_link = e.s_net_inject = 0;
     e.s_dram = e.s_bus_cont = e.s_flits = e.s_mg1 = e.s_lockdown = e.s_busacc = e.s_reqs = e.s_err = 0;
     e.s_bcast = 0;
+    e.pool_top = 0;
+    e.stop = false;
     for (uint64_t i = 0; i < n; i++) {
         uint64_t d = e.transmit(src[i], dst[i], len[i], timer[i]);
         if (e.ln == 0) out[i] = d;
@@ -891,7 +1072,29 @@ __global__ __launch_bounds__(64) void unit_network_kernel(const Geo* __restrict_
     e.flush_stats();
 }
 
+// Sharer-bitmap pool: free stack [0, P) and RunState.pool_top = P per replica.
+__global__ void init_pool_kernel(char* arena, uint64_t replica_bytes, uint64_t off_pool_free, uint64_t off_run,
+                                 int pool_entries, int nreplicas) {
+    uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t total = (uint64_t)pool_entries * (uint64_t)nreplicas;
+    if (id >= total) return;
+    uint64_t r = id / (uint64_t)pool_entries, k = id % (uint64_t)pool_entries;
+    char* base = arena + r * replica_bytes;
+    reinterpret_cast<int32_t*>(base + off_pool_free)[k] = (int32_t)k;
+    if (k == 0) reinterpret_cast<RunState*>(base + off_run)->pool_top = pool_entries;
+}
+
 }  // namespace
+
+extern "C" int pu_engine_init_pool(char* arena, uint64_t replica_bytes, uint64_t off_pool_free, uint64_t off_run,
+                                   int pool_entries, int nreplicas, hipStream_t stream) {
+    uint64_t total = (uint64_t)pool_entries * (uint64_t)nreplicas;
+    if (total == 0) return 0;
+    unsigned blocks = (unsigned)((total + 255) / 256);
+    hipLaunchKernelGGL(init_pool_kernel, dim3(blocks), dim3(256), 0, stream, arena, replica_bytes, off_pool_free,
+                       off_run, pool_entries, nreplicas);
+    return hipGetLastError() == hipSuccess ? 0 : PU_EIO;
+}
 
 extern "C" int pu_engine_unit_queue(const Geo* d_geo, char* base, uint64_t minp, const uint64_t* t,
                                     const uint64_t* p, uint64_t n, uint64_t* out, uint64_t* mg1, hipStream_t s) {

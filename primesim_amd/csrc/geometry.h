@@ -10,10 +10,12 @@
 //     alive[l] : ncaches x u32 (reference creates caches lazily, system.cpp:172)
 //     cnt[l]   : ncaches x 4 x u64 (ins, miss, evict, wb)
 //   directory / shared-LLC slices (one per network node):
-//     dmeta, dts          : N*nsets*nways lines
-//     dsh                 : N*nsets*nways x nwords x u64 full-map sharer bitmap
-//                           (replaces std::set<int>, iterated in ascending id)
-//     dalive, dcnt        : per slice
+//     dline    : N*nsets*nways x DirLine (32 B: tag, prog, state, sharers, ts)
+//                sharers (std::set<int> in the reference, iterated ascending)
+//                are held inline as up to 4 sorted 16-bit ids; a larger set
+//                moves to a full-map bitmap taken from a per-replica pool
+//     pool     : pool_entries x nwords x u64 bitmaps + a free stack
+//     dalive, dcnt : per slice
 //   queues (Graphite history tree restated as a ring of sorted free intervals):
 //     qhdr : nqueues x QueueHdr (64 B)   — links first, then per-cache buses
 //     qring: nqueues x 128 x {first,second} (2 KB)
@@ -38,6 +40,19 @@ struct LineMeta {
     int32_t id;
     uint32_t state;
 };
+
+// Directory / shared-LLC line (reference Line, cache.h:77-87, with sharer_set).
+struct DirLine {
+    uint64_t tag;
+    int32_t id;
+    uint8_t state;
+    uint8_t nsh;       // 0..4 inline sharers in `sh`; PU_SH_POOL: `sh` is a pool index
+    uint16_t _pad;
+    uint64_t sh;       // inline: ids (16 bits each) ascending from bit 0
+    int64_t ts;
+};
+#define PU_SH_INLINE 4
+#define PU_SH_POOL 0xFF
 
 struct QueueHdr {
     uint32_t head;
@@ -73,7 +88,8 @@ struct LevelGeo {
 struct DirGeo {
     uint64_t nsets, nways, block;
     int32_t offbits, idxbits, access_time, nwords;
-    uint64_t off_meta, off_ts, off_sh, off_alive, off_cnt;
+    int32_t pool_entries, _pad;
+    uint64_t off_line, off_pool, off_pool_free, off_alive, off_cnt;
 };
 
 struct Geo {
@@ -96,4 +112,6 @@ struct RunState {
                            // prints an error and exits the handler thread, so no
                            // further request reaches the uncore
     uint64_t processed;    // requests processed so far
+    int32_t pool_top;      // free entries on the sharer-bitmap pool stack
+    int32_t _pad;
 };

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -27,6 +28,8 @@
 
 extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,
                                 const pu_req* reqs, const uint64_t* off, int32_t* delays, hipStream_t stream);
+extern "C" int pu_engine_init_pool(char* arena, uint64_t replica_bytes, uint64_t off_pool_free, uint64_t off_run,
+                                   int pool_entries, int nreplicas, hipStream_t stream);
 extern "C" int pu_engine_unit_queue(const Geo* d_geo, char* base, uint64_t minp, const uint64_t* t,
                                     const uint64_t* p, uint64_t n, uint64_t* out, uint64_t* mg1, hipStream_t s);
 extern "C" int pu_engine_unit_network(const Geo* d_geo, char* base, const int32_t* src, const int32_t* dst,
@@ -156,9 +159,16 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
         L.off_cnt = lay.take((uint64_t)L.ncaches * 32);
     }
     uint64_t dlines = (uint64_t)N * D.nsets * D.nways;
-    D.off_meta = lay.take(dlines * sizeof(LineMeta));
-    D.off_ts = lay.take(dlines * sizeof(int64_t));
-    D.off_sh = lay.take(dlines * (uint64_t)D.nwords * 8);
+    D.off_line = lay.take(dlines * sizeof(DirLine));
+    // sharer sets of more than 4 LLCs live in pool bitmaps: one entry per 64
+    // directory lines by default (PRIMEUNCORE_POOL_ENTRIES overrides); running
+    // out stops the replica with PU_ERRF_POOL rather than diverge
+    uint64_t pool = dlines / 64 < 64 ? 64 : dlines / 64;
+    if (const char* e = std::getenv("PRIMEUNCORE_POOL_ENTRIES")) pool = std::strtoull(e, nullptr, 10);
+    if (pool > (1ull << 30)) pool = 1ull << 30;
+    D.pool_entries = (int32_t)pool;
+    D.off_pool = lay.take(pool * (uint64_t)D.nwords * 8);
+    D.off_pool_free = lay.take(pool * 4);
     D.off_alive = lay.take((uint64_t)N * 4);
     D.off_cnt = lay.take((uint64_t)N * 32);
     g->off_qhdr = lay.take((uint64_t)g->nqueues * sizeof(QueueHdr));
@@ -209,6 +219,9 @@ int reset_state(pu_handle* h) {
     int rc = pu_engine_init_queues(h->arena, h->geo.replica_bytes, h->geo.off_qhdr, h->geo.off_qring,
                                    h->geo.nqueues, h->R, h->stream);
     if (rc) return pu::set_error(rc, "queue init launch failed");
+    rc = pu_engine_init_pool(h->arena, h->geo.replica_bytes, h->geo.dir.off_pool_free, h->geo.off_run,
+                             h->geo.dir.pool_entries, h->R, h->stream);
+    if (rc) return pu::set_error(rc, "pool init launch failed");
     HIP_TRY(hipStreamSynchronize(h->stream), PU_EIO);
     return 0;
 }
