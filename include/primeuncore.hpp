@@ -1,0 +1,122 @@
+// primeuncore.hpp — header-only C++ mirror of the reference's UncoreManager
+// (reference src/uncore_manager.h:51-68) over the C ABI in primeuncore.h.
+//
+// A maintainer swaps `UncoreManager uncore_manager;` (reference prime.h:63) for
+// `pu::UncoreManager uncore_manager;` and keeps the call sites; the per-message
+// loop of prime.cpp:120-137 can instead hand the whole message to
+// access_message() (one engine launch per message).  See INTEGRATION.md.
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <ostream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "primeuncore.h"
+
+namespace pu {
+
+// The fields of the reference InsMem (cache.h:92-99) that System::access reads.
+struct InsMem {
+    char mem_type;       // 0 read, 1 write
+    int prog_id;
+    int thread_id;
+    int rec_thread_id;
+    uint64_t addr_dmem;  // updated in place like System::access (system.cpp:916)
+};
+
+class UncoreManager {
+   public:
+    UncoreManager() = default;
+    UncoreManager(const UncoreManager&) = delete;
+    UncoreManager& operator=(const UncoreManager&) = delete;
+    ~UncoreManager() { pu_destroy(h_); }
+
+    // UncoreManager::init (uncore_manager.cpp:46-50); `replicas` independent uncores.
+    void init(const pu_sim_cfg* cfg, int replicas = 1, int device = 0) {
+        h_ = pu_create(cfg, replicas, device);
+        if (!h_) throw std::runtime_error(std::string("pu_create: ") + pu_last_error());
+        num_cores_ = cfg->sys.num_cores;
+    }
+    // XmlParser::parse (xml_parser.cpp:684) + init.
+    void init_from_xml(const char* path, int replicas = 1, int device = 0) {
+        pu_sim_cfg cfg;
+        if (pu_config_load_xml(path, &cfg) != 0) throw std::runtime_error(pu_last_error());
+        init(&cfg, replicas, device);
+    }
+
+    int allocCore(int prog_id, int thread_id) { return pu_alloc_core(h_, prog_id, thread_id); }
+    int deallocCore(int prog_id, int thread_id) { return pu_dealloc_core(h_, prog_id, thread_id); }
+    int getCoreId(int prog_id, int thread_id) { return pu_get_core_id(h_, prog_id, thread_id); }
+
+    // UncoreManager::uncore_access (uncore_manager.cpp:82-85): -1 if core_id >= num_cores.
+    int uncore_access(int core_id, InsMem* ins, int64_t timer) {
+        return pu_access(h_, core_id, ins->prog_id, ins->mem_type, &ins->addr_dmem, timer);
+    }
+
+    // One MEM_REQUESTS message (prime.cpp:120-137): returns the `delay` prime.cpp
+    // sends back (sum of (d_i - 1)), or throws on engine errors.
+    int access_message(int core_id, int prog_id, const bool* mem_type, const uint64_t* addr,
+                       const int64_t* timer, size_t n, int replica = 0) {
+        static_assert(sizeof(bool) == sizeof(char), "MsgMem bool is one byte");
+        reqs_.resize(n);
+        delays_.resize(n);
+        for (size_t i = 0; i < n; i++) {
+            pu_req& r = reqs_[i];
+            r = pu_req{};
+            r.addr = addr[i];
+            r.timer = timer[i];
+            r.core = core_id;
+            r.prog_id = prog_id;
+            r.mem_type = mem_type[i] ? PU_WR : PU_RD;
+            r.batch_start = i == 0;
+        }
+        if (pu_access_batch(h_, replica, reqs_.data(), n, delays_.data()) != 0)
+            throw std::runtime_error(pu_last_error());
+        int delay = 0;
+        for (size_t i = 0; i < n; i++) delay += delays_[i] - 1;
+        return delay;
+    }
+
+    // Same, reading the reference's MsgMem wire records (common.h:49-59: bool mem_type;
+    // int mem_size; uint64_t addr_dmem; int64_t timer — 24 bytes) directly, e.g.
+    // access_msgmem(core_id, MPI_SOURCE, &msg_mem[index_prev][1], msg_len - 1).
+    int access_msgmem(int core_id, int prog_id, const void* records, size_t n, int replica = 0) {
+        const unsigned char* p = static_cast<const unsigned char*>(records);
+        types_.resize(n);
+        addrs_.resize(n);
+        timers_.resize(n);
+        for (size_t i = 0; i < n; i++, p += 24) {
+            types_[i] = p[0] != 0;
+            std::memcpy(&addrs_[i], p + 8, 8);
+            std::memcpy(&timers_[i], p + 16, 8);
+        }
+        return access_message(core_id, prog_id, reinterpret_cast<const bool*>(types_.data()), addrs_.data(),
+                              timers_.data(), n, replica);
+    }
+
+    // UncoreManager::report (uncore_manager.cpp:87-98).
+    void report(std::ostream* out, int replica = 0) {
+        long n = pu_report(h_, replica, 1, nullptr, 0);
+        if (n < 0) throw std::runtime_error(pu_last_error());
+        std::string buf((size_t)n + 1, '\0');
+        pu_report(h_, replica, 1, &buf[0], buf.size());
+        buf.resize((size_t)n);
+        *out << buf;
+    }
+
+    pu_handle* handle() { return h_; }
+
+   private:
+    pu_handle* h_ = nullptr;
+    int num_cores_ = 0;
+    std::vector<pu_req> reqs_;
+    std::vector<int32_t> delays_;
+    std::vector<char> types_;
+    std::vector<uint64_t> addrs_;
+    std::vector<int64_t> timers_;
+};
+
+}  // namespace pu

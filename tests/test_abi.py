@@ -72,3 +72,24 @@ def test_stream_api_errors():
     from primesim_amd import _abi as A
     p = A.StreamParams(99, 16, 1, 1000, 1, 100, 1, 0, -1, 0)
     assert lib().pu_stream_count(C.byref(p)) < 0
+
+
+def test_cpp_mirror_header_compiles(tmp_path):
+    """include/primeuncore.hpp (the UncoreManager mirror a prime.cpp build would use) compiles and links."""
+    import shutil
+    import subprocess
+    if not shutil.which("g++"):
+        pytest.skip("no g++")
+    src = tmp_path / "use.cpp"
+    src.write_text(
+        '#include "primeuncore.hpp"\n'
+        '#include <sstream>\n'
+        'int main(){ pu::UncoreManager m; pu_sim_cfg c{}; (void)c; std::ostringstream o;\n'
+        '  if (0) { m.init(&c); pu::InsMem i{0,1,0,0,64}; m.uncore_access(0,&i,1);\n'
+        '    char rec[48] = {0}; m.access_msgmem(0,1,rec,2); m.report(&o); }\n'
+        '  return 0; }\n')
+    out = tmp_path / "use"
+    r = subprocess.run(["g++", "-std=c++17", f"-I{ROOT}/include", str(src), "-o", str(out),
+                        f"-L{ROOT}/primesim_amd", "-lprimeuncore", f"-Wl,-rpath,{ROOT}/primesim_amd"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
