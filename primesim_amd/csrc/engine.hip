@@ -102,6 +102,348 @@ struct RouteView {
     uint64_t f0, f1;     // ring[head].first, ring[head+1].first
 };
 
+#define AS1 __attribute__((address_space(1)))
+// native vectors (not classes), so loads/stores through global-address-space
+// pointers need no conversion: slot = {first, second}, header = 10 dwords
+typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+
+// Per-wave statistics in LDS (one workgroup = one wave = one replica); lane 0
+// adds with ds_add_u64 (no return, no wait) and the kernel flushes once.
+enum StatId {
+    SN_ACC, SN_DIST, SN_TOTAL, SN_ROUTER, SN_LINK, SN_INJECT, SN_DRAM, SN_BUSCONT, SN_FLITS, SN_MG1,
+    SN_LOCKDOWN, SN_BUSACC, SN_REQS, SN_BCAST, SN_COUNT
+};
+static __shared__ unsigned long long lds_stat[SN_COUNT];
+static __shared__ unsigned long long lds_err;
+
+__device__ __forceinline__ void stat_add(int k, uint64_t v) {
+    if (lane_id() == 0) atomicAdd(&lds_stat[k], (unsigned long long)v);
+}
+__device__ __forceinline__ void err_or(uint64_t f) {
+    if (lane_id() == 0) atomicOr(&lds_err, (unsigned long long)f);
+}
+
+// Wave-uniform context of the queue/network code (all values in SGPRs).
+struct NetCtx {
+    AS1 char* base;            // replica arena
+    uint64_t off_qhdr, off_qring;
+    uint64_t router, link_delay, inject;
+    int header_flits, data_width, w, net_type;
+};
+
+__device__ __forceinline__ AS1 v2u64* q_ring(const NetCtx& c, int q) {
+    return reinterpret_cast<AS1 v2u64*>(c.base + c.off_qring) + (size_t)q * PU_QRING;
+}
+__device__ __forceinline__ AS1 uint32_t* q_hdr(const NetCtx& c, int q) {
+    return reinterpret_cast<AS1 uint32_t*>(c.base + c.off_qhdr + (uint64_t)q * sizeof(QueueHdr));
+}
+
+// M/G/1 (queue_model_m_g_1.cpp:16-42), reference operation order.
+__device__ __forceinline__ uint64_t mg1_wait(const QState& s) {
+    if (s.n == 0) return 0;
+    double nd = (double)s.n;
+    double mean = s.sum / nd;
+    double var = (s.sum_sq / nd) - mean * mean;
+    double mu = 1.0 / mean;
+    double lambda = nd / (double)s.newest;
+    if (lambda >= mu) lambda = 0.999 * mu;
+    double inv = 1.0 / (mu * mu);
+    double num = 0.5 * mu;
+    num = num * lambda;
+    num = num * (inv + var);
+    double w = num / (mu - lambda);
+    return (uint64_t)ceil(w);
+}
+
+// Tree branch of QueueModelHistoryTree::computeQueueDelay
+// (queue_model_history_tree.cpp:64-112) on the full ring.  head/cnt are the
+// post-prune values and are updated; edited slots are written back.
+__device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingView& v, uint32_t& head,
+                                            uint32_t& cnt, uint64_t t, uint64_t p, uint64_t minp, uint64_t& err) {
+    const int ln = lane_id();
+    const uint64_t tp = t + p;
+    const uint32_t jl = ((uint32_t)ln - head) & (PU_QRING - 1);
+    const uint32_t jh = ((uint32_t)ln + 64 - head) & (PU_QRING - 1);
+    bool pl = jl < cnt && ((v.lf <= t && tp <= v.ls) || (t < v.lf && v.ls - v.lf >= p));
+    bool ph = jh < cnt && ((v.hf <= t && tp <= v.hs) || (t < v.hf && v.hs - v.hf >= p));
+    uint64_t ml = ballot(pl), mh = ballot(ph);
+    // leftmost interval in logical (ring) order starting at `head`
+    uint32_t slot;
+    if (head < 64) {
+        uint64_t ge = ml & (~0ull << head);
+        if (ge) slot = (uint32_t)__builtin_ctzll(ge);
+        else if (mh) slot = 64 + (uint32_t)__builtin_ctzll(mh);
+        else slot = (uint32_t)__builtin_ctzll(ml);
+    } else {
+        uint64_t ge = mh & (~0ull << (head - 64));
+        if (ge) slot = 64 + (uint32_t)__builtin_ctzll(ge);
+        else if (ml) slot = (uint32_t)__builtin_ctzll(ml);
+        else slot = 64 + (uint32_t)__builtin_ctzll(mh);
+    }
+    if ((ml | mh) == 0) {      // search returned NULL: an assert in the reference
+        err |= PU_ERRF_QUEUE;
+        slot = head;
+    }
+    const uint32_t k = (slot - head) & (PU_QRING - 1);
+    const uint64_t f = slot < 64 ? rl64(v.lf, (int)slot) : rl64(v.hf, (int)(slot - 64));
+    const uint64_t s = slot < 64 ? rl64(v.ls, (int)slot) : rl64(v.hs, (int)(slot - 64));
+    uint64_t d;
+    int op;  // 1 second<-t, 2 first<-nf, 3 remove, 4 split
+    uint64_t nf = 0;
+    if (t >= f) {
+        d = 0;
+        if (t - f >= minp) {
+            op = (s - tp >= minp) ? 4 : 1;
+        } else if (s - tp >= minp) {
+            op = 2;
+            nf = tp;
+        } else {
+            op = 3;
+        }
+    } else {
+        d = f - t;
+        if (s - (f + p) >= minp) {
+            op = 2;
+            nf = f + p;
+        } else {
+            op = 3;
+        }
+    }
+    bool dl = false, dh = false;
+    uint64_t lf = v.lf, ls = v.ls, hf = v.hf, hs = v.hs;
+    if (op == 1 || op == 2) {
+        if (jl == k) { if (op == 1) ls = t; else lf = nf; dl = true; }
+        if (jh == k) { if (op == 1) hs = t; else hf = nf; dh = true; }
+    } else if (op == 3) {
+        if (k == 0) {
+            head = (head + 1) & (PU_QRING - 1);
+        } else {
+            // logical [k+1, cnt) move down one: slot s takes slot s+1
+            const int src = (ln + 1) & 63;
+            uint64_t a_f = shfl64(v.lf, src), a_s = shfl64(v.ls, src);
+            uint64_t b_f = shfl64(v.hf, src), b_s = shfl64(v.hs, src);
+            uint64_t sl_f = ln == 63 ? b_f : a_f, sl_s = ln == 63 ? b_s : a_s;
+            uint64_t sh_f = ln == 63 ? a_f : b_f, sh_s = ln == 63 ? a_s : b_s;
+            if (jl >= k && jl + 1 < cnt) { lf = sl_f; ls = sl_s; dl = true; }
+            if (jh >= k && jh + 1 < cnt) { hf = sh_f; hs = sh_s; dh = true; }
+        }
+        cnt = cnt - 1;
+    } else {  // split: node k keeps [first, t]; [t+p, second] inserted at k+1
+        const int src = (ln + 63) & 63;
+        uint64_t a_f = shfl64(v.lf, src), a_s = shfl64(v.ls, src);
+        uint64_t b_f = shfl64(v.hf, src), b_s = shfl64(v.hs, src);
+        uint64_t pl_f = ln == 0 ? b_f : a_f, pl_s = ln == 0 ? b_s : a_s;
+        uint64_t ph_f = ln == 0 ? a_f : b_f, ph_s = ln == 0 ? a_s : b_s;
+        if (jl == k) { ls = t; dl = true; }
+        else if (jl == k + 1) { lf = tp; ls = s; dl = true; }
+        else if (jl >= k + 2 && jl <= cnt) { lf = pl_f; ls = pl_s; dl = true; }
+        if (jh == k) { hs = t; dh = true; }
+        else if (jh == k + 1) { hf = tp; hs = s; dh = true; }
+        else if (jh >= k + 2 && jh <= cnt) { hf = ph_f; hs = ph_s; dh = true; }
+        cnt = cnt + 1;
+    }
+    AS1 v2u64* R = q_ring(c, q);
+    if (dl) R[ln] = v2u64{lf, ls};
+    if (dh) R[ln + 64] = v2u64{hf, hs};
+    return d;
+}
+
+// M/G/1 update (queue_model_m_g_1.cpp:45-55) and header write-back (lane 0).
+__device__ __forceinline__ void q_finish(const NetCtx& c, int q, QState& st, uint64_t t, uint64_t p, uint64_t d) {
+    st.sum_sq = st.sum_sq + (double)p * (double)p;
+    st.sum = st.sum + (double)p;
+    st.n = st.n + 1;
+    uint64_t fin = t + d + p;
+    st.newest = fin > st.newest ? fin : st.newest;
+    if (lane_id() == 0) {
+        AS1 uint32_t* H = q_hdr(c, q);
+        uint64_t sb = (uint64_t)__double_as_longlong(st.sum), qb = (uint64_t)__double_as_longlong(st.sum_sq);
+        *reinterpret_cast<AS1 v4u32*>(H) = v4u32{st.head, st.count, (uint32_t)st.n, (uint32_t)(st.n >> 32)};
+        *reinterpret_cast<AS1 v4u32*>(H + 4) =
+            v4u32{(uint32_t)sb, (uint32_t)(sb >> 32), (uint32_t)qb, (uint32_t)(qb >> 32)};
+        *reinterpret_cast<AS1 v2u32*>(H + 8) = v2u32{(uint32_t)st.newest, (uint32_t)(st.newest >> 32)};
+    }
+}
+
+// One computeQueueDelay given the header and the first two interval starts.
+__device__ __forceinline__ uint64_t q_step(const NetCtx& c, int q, QState& st, uint64_t f0, uint64_t f1, uint64_t t,
+                                           uint64_t p, uint64_t minp, uint64_t& mg1, uint64_t& err) {
+    uint64_t front = f0;
+    if (st.count >= PU_QMAX) {      // prune the minimum (history_tree.cpp:49-55)
+        st.head = (st.head + 1) & (PU_QRING - 1);
+        st.count--;
+        front = f1;
+    }
+    uint64_t d;
+    if (front > t + p) {             // older than the tracked history: M/G/1 (history_tree.cpp:58-63)
+        d = mg1_wait(st);
+        mg1++;
+    } else {
+        const AS1 v2u64* R = q_ring(c, q);
+        const int ln = lane_id();
+        v2u64 a = R[ln], b = R[ln + 64];
+        RingView v{a.x, a.y, b.x, b.y};
+        d = tree_op(c, q, v, st.head, st.count, t, p, minp, err);
+    }
+    q_finish(c, q, st, t, p, d);
+    return d;
+}
+
+__device__ __forceinline__ QState hdr_state(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t d4,
+                                            uint32_t d5, uint32_t d6, uint32_t d7, uint32_t d8, uint32_t d9) {
+    QState st;
+    st.head = d0;
+    st.count = d1;
+    st.n = ((uint64_t)d3 << 32) | d2;
+    st.sum = __longlong_as_double((long long)(((uint64_t)d5 << 32) | d4));
+    st.sum_sq = __longlong_as_double((long long)(((uint64_t)d7 << 32) | d6));
+    st.newest = ((uint64_t)d9 << 32) | d8;
+    return st;
+}
+
+// A whole queue op loading its own state (bus queues, unit tests).
+__device__ __forceinline__ uint64_t q_op(const NetCtx& c, int q, uint64_t t, uint64_t p, uint64_t minp, uint64_t& mg1,
+                                         uint64_t& err) {
+    const AS1 uint32_t* H = q_hdr(c, q);
+    v4u32 a = *reinterpret_cast<const AS1 v4u32*>(H);
+    v4u32 b = *reinterpret_cast<const AS1 v4u32*>(H + 4);
+    v2u32 e = *reinterpret_cast<const AS1 v2u32*>(H + 8);
+    QState st = hdr_state(uni32(a.x), uni32(a.y), uni32(a.z), uni32(a.w), uni32(b.x), uni32(b.y), uni32(b.z),
+                          uni32(b.w), uni32(e.x), uni32(e.y));
+    const AS1 v2u64* R = q_ring(c, q);
+    uint64_t f0 = uni64(R[st.head].x), f1 = uni64(R[(st.head + 1) & (PU_QRING - 1)].x);
+    return q_step(c, q, st, f0, f1, t, p, minp, mg1, err);
+}
+
+__device__ __forceinline__ void net_coords(const NetCtx& c, int id, int& x, int& y, int& z) {
+    const int w = c.w;
+    if (c.net_type == 1) {
+        x = (id % (w * w)) % w;
+        y = (id % (w * w)) / w;
+        z = id / (w * w);
+    } else {
+        x = id % w;
+        y = id / w;
+        z = 0;
+    }
+}
+// Network::getLink (network.cpp:213-307): one record per undirected edge.
+__device__ __forceinline__ int net_link(const NetCtx& c, int x, int y, int z, int dir) {
+    const int w = c.w;
+    int a, b, cc;
+    if (c.net_type == 1) {
+        switch (dir) {
+            case 0: a = x; b = y; cc = z; break;
+            case 1: a = x - 1; b = y; cc = z; break;
+            case 2: a = y - 1; b = z; cc = x + w; break;
+            case 3: a = y; b = z; cc = x + w; break;
+            case 4: a = z; b = x; cc = y + 2 * w; break;
+            default: a = z - 1; b = x; cc = y + 2 * w; break;
+        }
+        return (a * w + b) * (3 * w) + cc;
+    }
+    switch (dir) {
+        case 0: a = x; b = y; break;
+        case 1: a = x - 1; b = y; break;
+        case 2: a = y - 1; b = x + w; break;
+        default: a = y; b = x + w; break;
+    }
+    return a * (2 * w) + b;
+}
+// link of hop h of the X-then-Y-then-Z route from (sx,sy,sz) to (rx,ry,rz)
+__device__ __forceinline__ int net_route_link(const NetCtx& c, int h, int sx, int sy, int sz, int rx, int ry, int rz,
+                                              int hx, int hy) {
+    if (h < hx) {
+        int e = rx > sx;
+        int x = e ? sx + h : sx - h;
+        return net_link(c, x, sy, sz, e ? 0 : 1);
+    }
+    if (h < hx + hy) {
+        int s = ry > sy;
+        int y = s ? sy + (h - hx) : sy - (h - hx);
+        return net_link(c, rx, y, sz, s ? 3 : 2);
+    }
+    int u = rz > sz;
+    int z = u ? sz + (h - hx - hy) : sz - (h - hx - hy);
+    return net_link(c, rx, ry, z, u ? 4 : 5);
+}
+
+// Network::transmit (network.cpp:97-160).  Out of line (one copy), every
+// argument made wave-uniform so the hop loop runs on SGPRs and scalar branches.
+// Lane h prefetches hop h's link header and the two interval starts at its
+// ring head; only hops taking the tree branch fetch their full ring.
+__device__ __noinline__ uint64_t net_transmit(char* base_in, uint64_t off_qhdr, uint64_t off_qring, uint64_t router,
+                                              uint64_t link_delay, uint64_t inject, int header_flits, int data_width,
+                                              int w, int net_type, int src, int dst, int len, uint64_t timer) {
+    NetCtx c;
+    c.base = (AS1 char*)(char*)uni64((uint64_t)base_in);
+    c.off_qhdr = uni64(off_qhdr);
+    c.off_qring = uni64(off_qring);
+    c.router = uni64(router);
+    c.link_delay = uni64(link_delay);
+    c.inject = uni64(inject);
+    c.header_flits = (int)uni32((uint32_t)header_flits);
+    c.data_width = (int)uni32((uint32_t)data_width);
+    c.w = (int)uni32((uint32_t)w);
+    c.net_type = (int)uni32((uint32_t)net_type);
+    src = (int)uni32((uint32_t)src);
+    dst = (int)uni32((uint32_t)dst);
+    len = (int)uni32((uint32_t)len);
+    timer = uni64(timer);
+    if (src == dst) return 0;
+    const int ln = lane_id();
+    const int plen = c.header_flits + (int)ceil((double)len / (double)c.data_width);
+    int sx, sy, sz, rx, ry, rz;
+    net_coords(c, src, sx, sy, sz);
+    net_coords(c, dst, rx, ry, rz);
+    const int hx = abs(rx - sx), hy = abs(ry - sy), hz = abs(rz - sz);
+    const int hops = hx + hy + hz;
+    uint64_t t = timer + c.inject;
+    uint64_t mg1 = 0, err = 0;
+    for (int b0 = 0; b0 < hops; b0 += 64) {
+        // ---- prefetch the window: lane h = hop b0+h
+        const int h = b0 + ln;
+        int rq = 0;
+        v4u32 ha = v4u32{0, 0, 0, 0}, hb = v4u32{0, 0, 0, 0};
+        v2u32 hc = v2u32{0, 0};
+        uint64_t rf0 = 0, rf1 = 0;
+        if (h < hops) {
+            rq = net_route_link(c, h, sx, sy, sz, rx, ry, rz, hx, hy);
+            const AS1 uint32_t* H = q_hdr(c, rq);
+            ha = *reinterpret_cast<const AS1 v4u32*>(H);
+            hb = *reinterpret_cast<const AS1 v4u32*>(H + 4);
+            hc = *reinterpret_cast<const AS1 v2u32*>(H + 8);
+            const AS1 v2u64* R = q_ring(c, rq);
+            rf0 = R[ha.x].x;
+            rf1 = R[(ha.x + 1) & (PU_QRING - 1)].x;
+        }
+        const int nh = hops - b0 < 64 ? hops - b0 : 64;
+        for (int j = 0; j < nh; j++) {
+            t += c.router;
+            const int q = (int)rl32((uint32_t)rq, j);
+            QState st = hdr_state(rl32(ha.x, j), rl32(ha.y, j), rl32(ha.z, j), rl32(ha.w, j), rl32(hb.x, j),
+                                  rl32(hb.y, j), rl32(hb.z, j), rl32(hb.w, j), rl32(hc.x, j), rl32(hc.y, j));
+            t += q_step(c, q, st, rl64(rf0, j), rl64(rf1, j), t, (uint64_t)plen, c.link_delay, mg1, err) +
+                 c.link_delay;
+        }
+    }
+    t += c.router;
+    t += (uint64_t)(plen - 1);
+    const uint64_t dist = (uint64_t)hops;
+    stat_add(SN_ACC, 1);
+    stat_add(SN_TOTAL, t - timer);
+    stat_add(SN_ROUTER, (dist + 1) * c.router);
+    stat_add(SN_LINK, t - timer - (dist + 1) * c.router - (uint64_t)(plen - 1) - c.inject);
+    stat_add(SN_INJECT, c.inject);
+    stat_add(SN_DIST, dist);
+    stat_add(SN_FLITS, dist * (uint64_t)plen);
+    stat_add(SN_MG1, mg1);
+    if (err) err_or(err);
+    return t - timer;
+}
+
 template <int NL>
 struct Engine {
     const Geo* __restrict__ g;
@@ -114,319 +456,30 @@ struct Engine {
     int32_t pool_top;    // sharer-bitmap pool stack (RunState.pool_top)
     bool stop;           // replica must stop (pool exhausted)
 
-    // stats accumulated in registers, flushed once per launch
-    uint64_t s_net_acc, s_net_dist, s_net_total, s_net_router, s_net_link, s_net_inject;
-    uint64_t s_dram, s_bus_cont, s_flits, s_mg1, s_lockdown, s_busacc, s_reqs, s_err;
-    int64_t s_bcast;
 
     template <class T>
     __device__ __forceinline__ T* at(uint64_t off) const {
         return reinterpret_cast<T*>(base + off);
     }
 
-    // ------------------------------------------------------------ queues
-    __device__ __forceinline__ QueueSlot* ring_of(int q) const {
-        return at<QueueSlot>(g->off_qring) + (size_t)q * PU_QRING;
-    }
-    __device__ __forceinline__ void ring_load(RingView& v, int q) const {
-        const QueueSlot* R = ring_of(q);
-        QueueSlot a = R[ln];
-        QueueSlot b = R[ln + 64];
-        v.lf = a.first; v.ls = a.second;
-        v.hf = b.first; v.hs = b.second;
-    }
-
-    // M/G/1 (queue_model_m_g_1.cpp:16-42), reference operation order.
-    __device__ __forceinline__ uint64_t mg1_wait(const QState& s) const {
-        if (s.n == 0) return 0;
-        double nd = (double)s.n;
-        double mean = s.sum / nd;
-        double var = (s.sum_sq / nd) - mean * mean;
-        double mu = 1.0 / (s.sum / nd);
-        double lambda = nd / (double)s.newest;
-        if (lambda >= mu) lambda = 0.999 * mu;
-        double inv = 1.0 / (mu * mu);
-        double num = 0.5 * mu;
-        num = num * lambda;
-        num = num * (inv + var);
-        double w = num / (mu - lambda);
-        return (uint64_t)ceil(w);
-    }
-
-    // Tree branch of QueueModelHistoryTree::computeQueueDelay
-    // (queue_model_history_tree.cpp:64-112) on the full ring.  head/cnt are the
-    // post-prune values and are updated; edited slots are written back.
-    __device__ uint64_t tree_op(int q, const RingView& v, uint32_t& head, uint32_t& cnt, uint64_t t, uint64_t p,
-                                uint64_t minp) {
-        const uint64_t tp = t + p;
-        const uint32_t jl = ((uint32_t)ln - head) & (PU_QRING - 1);
-        const uint32_t jh = ((uint32_t)ln + 64 - head) & (PU_QRING - 1);
-        bool pl = jl < cnt && ((v.lf <= t && tp <= v.ls) || (t < v.lf && v.ls - v.lf >= p));
-        bool ph = jh < cnt && ((v.hf <= t && tp <= v.hs) || (t < v.hf && v.hs - v.hf >= p));
-        uint64_t ml = ballot(pl), mh = ballot(ph);
-        // leftmost interval in logical (ring) order starting at `head`
-        uint32_t slot;
-        if (head < 64) {
-            uint64_t ge = ml & (~0ull << head);
-            if (ge) slot = (uint32_t)__builtin_ctzll(ge);
-            else if (mh) slot = 64 + (uint32_t)__builtin_ctzll(mh);
-            else slot = (uint32_t)__builtin_ctzll(ml);
-        } else {
-            uint64_t ge = mh & (~0ull << (head - 64));
-            if (ge) slot = 64 + (uint32_t)__builtin_ctzll(ge);
-            else if (ml) slot = (uint32_t)__builtin_ctzll(ml);
-            else slot = 64 + (uint32_t)__builtin_ctzll(mh);
-        }
-        if ((ml | mh) == 0) {      // search returned NULL: an assert in the reference
-            s_err |= PU_ERRF_QUEUE;
-            slot = head;
-        }
-        const uint32_t k = (slot - head) & (PU_QRING - 1);
-        const uint64_t f = slot < 64 ? rl64(v.lf, (int)slot) : rl64(v.hf, (int)(slot - 64));
-        const uint64_t s = slot < 64 ? rl64(v.ls, (int)slot) : rl64(v.hs, (int)(slot - 64));
-        uint64_t d;
-        int op;  // 1 second<-t, 2 first<-nf, 3 remove, 4 split
-        uint64_t nf = 0;
-        if (t >= f) {
-            d = 0;
-            if (t - f >= minp) {
-                op = (s - tp >= minp) ? 4 : 1;
-            } else if (s - tp >= minp) {
-                op = 2;
-                nf = tp;
-            } else {
-                op = 3;
-            }
-        } else {
-            d = f - t;
-            if (s - (f + p) >= minp) {
-                op = 2;
-                nf = f + p;
-            } else {
-                op = 3;
-            }
-        }
-        bool dl = false, dh = false;
-        uint64_t lf = v.lf, ls = v.ls, hf = v.hf, hs = v.hs;
-        if (op == 1 || op == 2) {
-            if (jl == k) { if (op == 1) ls = t; else lf = nf; dl = true; }
-            if (jh == k) { if (op == 1) hs = t; else hf = nf; dh = true; }
-        } else if (op == 3) {
-            if (k == 0) {
-                head = (head + 1) & (PU_QRING - 1);
-            } else {
-                // logical [k+1, cnt) move down one: slot s takes slot s+1
-                const int src = (ln + 1) & 63;
-                uint64_t a_f = shfl64(v.lf, src), a_s = shfl64(v.ls, src);
-                uint64_t b_f = shfl64(v.hf, src), b_s = shfl64(v.hs, src);
-                uint64_t sl_f = ln == 63 ? b_f : a_f, sl_s = ln == 63 ? b_s : a_s;
-                uint64_t sh_f = ln == 63 ? a_f : b_f, sh_s = ln == 63 ? a_s : b_s;
-                if (jl >= k && jl + 1 < cnt) { lf = sl_f; ls = sl_s; dl = true; }
-                if (jh >= k && jh + 1 < cnt) { hf = sh_f; hs = sh_s; dh = true; }
-            }
-            cnt = cnt - 1;
-        } else {  // split: node k keeps [first, t]; [t+p, second] inserted at k+1
-            const int src = (ln + 63) & 63;
-            uint64_t a_f = shfl64(v.lf, src), a_s = shfl64(v.ls, src);
-            uint64_t b_f = shfl64(v.hf, src), b_s = shfl64(v.hs, src);
-            uint64_t pl_f = ln == 0 ? b_f : a_f, pl_s = ln == 0 ? b_s : a_s;
-            uint64_t ph_f = ln == 0 ? a_f : b_f, ph_s = ln == 0 ? a_s : b_s;
-            if (jl == k) { ls = t; dl = true; }
-            else if (jl == k + 1) { lf = tp; ls = s; dl = true; }
-            else if (jl >= k + 2 && jl <= cnt) { lf = pl_f; ls = pl_s; dl = true; }
-            if (jh == k) { hs = t; dh = true; }
-            else if (jh == k + 1) { hf = tp; hs = s; dh = true; }
-            else if (jh >= k + 2 && jh <= cnt) { hf = ph_f; hs = ph_s; dh = true; }
-            cnt = cnt + 1;
-        }
-        QueueSlot* R = ring_of(q);
-        if (dl) R[ln] = QueueSlot{lf, ls};
-        if (dh) R[ln + 64] = QueueSlot{hf, hs};
-        return d;
-    }
-
-    // M/G/1 update (queue_model_m_g_1.cpp:45-55) and header write-back.
-    __device__ __forceinline__ void q_finish(int q, QState& st, uint64_t t, uint64_t p, uint64_t d) {
-        st.sum_sq = st.sum_sq + (double)p * (double)p;
-        st.sum = st.sum + (double)p;
-        st.n = st.n + 1;
-        uint64_t fin = t + d + p;
-        st.newest = fin > st.newest ? fin : st.newest;
-        if (ln < 10) {
-            uint64_t sb = (uint64_t)__double_as_longlong(st.sum), qb = (uint64_t)__double_as_longlong(st.sum_sq);
-            uint32_t w;
-            switch (ln) {
-                case 0: w = st.head; break;
-                case 1: w = st.count; break;
-                case 2: w = (uint32_t)st.n; break;
-                case 3: w = (uint32_t)(st.n >> 32); break;
-                case 4: w = (uint32_t)sb; break;
-                case 5: w = (uint32_t)(sb >> 32); break;
-                case 6: w = (uint32_t)qb; break;
-                case 7: w = (uint32_t)(qb >> 32); break;
-                case 8: w = (uint32_t)st.newest; break;
-                default: w = (uint32_t)(st.newest >> 32); break;
-            }
-            reinterpret_cast<uint32_t*>(at<QueueHdr>(g->off_qhdr) + q)[ln] = w;
-        }
-    }
-
-    // One computeQueueDelay given the header and the first two interval starts.
-    __device__ __forceinline__ uint64_t q_step(int q, QState& st, uint64_t f0, uint64_t f1, uint64_t t, uint64_t p,
-                                               uint64_t minp) {
-        uint64_t front = f0;
-        if (st.count >= PU_QMAX) {      // prune the minimum (history_tree.cpp:49-55)
-            st.head = (st.head + 1) & (PU_QRING - 1);
-            st.count--;
-            front = f1;
-        }
-        uint64_t d;
-        if (front > t + p) {             // older than the tracked history: M/G/1 (history_tree.cpp:58-63)
-            d = mg1_wait(st);
-            s_mg1++;
-        } else {
-            RingView v;
-            ring_load(v, q);
-            d = tree_op(q, v, st.head, st.count, t, p, minp);
-        }
-        q_finish(q, st, t, p, d);
-        return d;
-    }
-
-    // A whole queue op loading its own state (bus queues, unit tests).
-    __device__ uint64_t q_op(int q, uint64_t t, uint64_t p, uint64_t minp) {
-        const uint32_t* H = reinterpret_cast<const uint32_t*>(at<QueueHdr>(g->off_qhdr) + q);
-        uint32_t hw = ln < 10 ? H[ln] : 0u;
-        QState st;
-        st.head = rl32(hw, 0);
-        st.count = rl32(hw, 1);
-        st.n = ((uint64_t)rl32(hw, 3) << 32) | rl32(hw, 2);
-        st.sum = __longlong_as_double((long long)(((uint64_t)rl32(hw, 5) << 32) | rl32(hw, 4)));
-        st.sum_sq = __longlong_as_double((long long)(((uint64_t)rl32(hw, 7) << 32) | rl32(hw, 6)));
-        st.newest = ((uint64_t)rl32(hw, 9) << 32) | rl32(hw, 8);
-        const QueueSlot* R = ring_of(q);
-        uint32_t h0 = st.head, h1 = (st.head + 1) & (PU_QRING - 1);
-        uint64_t f0 = R[h0].first, f1 = R[h1].first;
-        return q_step(q, st, uni64(f0), uni64(f1), t, p, minp);
-    }
-
     // ------------------------------------------------------------ network
-    __device__ __forceinline__ void coords(int id, int& x, int& y, int& z) const {
-        const int w = g->net_width;
-        if (g->net_type == 1) {
-            x = (id % (w * w)) % w;
-            y = (id % (w * w)) / w;
-            z = id / (w * w);
-        } else {
-            x = id % w;
-            y = id / w;
-            z = 0;
-        }
+    __device__ __forceinline__ NetCtx net_ctx() const {
+        NetCtx c;
+        c.base = (AS1 char*)base;
+        c.off_qhdr = g->off_qhdr;
+        c.off_qring = g->off_qring;
+        c.router = g->router_delay;
+        c.link_delay = g->link_delay;
+        c.inject = g->inject_delay;
+        c.header_flits = g->header_flits;
+        c.data_width = g->data_width;
+        c.w = g->net_width;
+        c.net_type = g->net_type;
+        return c;
     }
-    // Network::getLink (network.cpp:213-307): one record per undirected edge.
-    __device__ __forceinline__ int link_of(int x, int y, int z, int dir) const {
-        const int w = g->net_width;
-        int a, b, c;
-        if (g->net_type == 1) {
-            switch (dir) {
-                case 0: a = x; b = y; c = z; break;
-                case 1: a = x - 1; b = y; c = z; break;
-                case 2: a = y - 1; b = z; c = x + w; break;
-                case 3: a = y; b = z; c = x + w; break;
-                case 4: a = z; b = x; c = y + 2 * w; break;
-                default: a = z - 1; b = x; c = y + 2 * w; break;
-            }
-            return (a * w + b) * (3 * w) + c;
-        }
-        switch (dir) {
-            case 0: a = x; b = y; break;
-            case 1: a = x - 1; b = y; break;
-            case 2: a = y - 1; b = x + w; break;
-            default: a = y; b = x + w; break;
-        }
-        return a * (2 * w) + b;
-    }
-    // link of hop h of the X-then-Y-then-Z route from (sx,sy,sz) to (rx,ry,rz)
-    __device__ __forceinline__ int route_link(int h, int sx, int sy, int sz, int rx, int ry, int rz,
-                                              int hx, int hy) const {
-        if (h < hx) {
-            int e = rx > sx;
-            int x = e ? sx + h : sx - h;
-            return link_of(x, sy, sz, e ? 0 : 1);
-        }
-        if (h < hx + hy) {
-            int s = ry > sy;
-            int y = s ? sy + (h - hx) : sy - (h - hx);
-            return link_of(rx, y, sz, s ? 3 : 2);
-        }
-        int u = rz > sz;
-        int z = u ? sz + (h - hx - hy) : sz - (h - hx - hy);
-        return link_of(rx, ry, z, u ? 4 : 5);
-    }
-
-    // Prefetch hops [b0, b0+64) of a route: lane h loads hop b0+h's link
-    // header and the two interval starts at its ring head (two dependent
-    // loads per lane, all hops in flight together).
-    __device__ __forceinline__ void route_load(RouteView& rv, int b0, int hops, int sx, int sy, int sz, int rx,
-                                               int ry, int rz, int hx, int hy) const {
-        const int h = b0 + ln;
-        rv.q = 0;
-        rv.d0 = rv.d1 = rv.d2 = rv.d3 = rv.d4 = rv.d5 = rv.d6 = rv.d7 = rv.d8 = rv.d9 = 0;
-        rv.f0 = rv.f1 = 0;
-        if (h < hops) {
-            const int q = route_link(h, sx, sy, sz, rx, ry, rz, hx, hy);
-            rv.q = q;
-            const uint4* H = reinterpret_cast<const uint4*>(at<QueueHdr>(g->off_qhdr) + q);
-            uint4 a = H[0], b = H[1];
-            uint2 c = reinterpret_cast<const uint2*>(H + 2)[0];
-            rv.d0 = a.x; rv.d1 = a.y; rv.d2 = a.z; rv.d3 = a.w;
-            rv.d4 = b.x; rv.d5 = b.y; rv.d6 = b.z; rv.d7 = b.w;
-            rv.d8 = c.x; rv.d9 = c.y;
-            const QueueSlot* R = ring_of(q);
-            rv.f0 = R[a.x].first;
-            rv.f1 = R[(a.x + 1) & (PU_QRING - 1)].first;
-        }
-    }
-
-    // Network::transmit (network.cpp:97-160)
-    __device__ uint64_t transmit(int src, int dst, int len, uint64_t timer) {
-        if (src == dst) return 0;
-        const int plen = g->header_flits + (int)ceil((double)len / (double)g->data_width);
-        int sx, sy, sz, rx, ry, rz;
-        coords(src, sx, sy, sz);
-        coords(dst, rx, ry, rz);
-        const int hx = abs(rx - sx), hy = abs(ry - sy), hz = abs(rz - sz);
-        const int hops = hx + hy + hz;
-        const uint64_t router = g->router_delay, link_delay = g->link_delay;
-        uint64_t t = timer + g->inject_delay;
-        for (int b0 = 0; b0 < hops; b0 += 64) {
-            RouteView rv;
-            route_load(rv, b0, hops, sx, sy, sz, rx, ry, rz, hx, hy);
-            const int nh = hops - b0 < 64 ? hops - b0 : 64;
-            for (int j = 0; j < nh; j++) {
-                t += router;
-                const int q = (int)rl32((uint32_t)rv.q, j);
-                QState st;
-                st.head = rl32(rv.d0, j);
-                st.count = rl32(rv.d1, j);
-                st.n = ((uint64_t)rl32(rv.d3, j) << 32) | rl32(rv.d2, j);
-                st.sum = __longlong_as_double((long long)(((uint64_t)rl32(rv.d5, j) << 32) | rl32(rv.d4, j)));
-                st.sum_sq = __longlong_as_double((long long)(((uint64_t)rl32(rv.d7, j) << 32) | rl32(rv.d6, j)));
-                st.newest = ((uint64_t)rl32(rv.d9, j) << 32) | rl32(rv.d8, j);
-                t += q_step(q, st, rl64(rv.f0, j), rl64(rv.f1, j), t, (uint64_t)plen, link_delay) + link_delay;
-                s_flits += (uint64_t)plen;
-            }
-        }
-        t += router;
-        t += (uint64_t)(plen - 1);
-        const uint64_t dist = (uint64_t)hops;
-        s_net_acc++;
-        s_net_total += t - timer;
-        s_net_router += (dist + 1) * router;
-        s_net_link += t - timer - (dist + 1) * router - (uint64_t)(plen - 1) - g->inject_delay;
-        s_net_inject += g->inject_delay;
-        s_net_dist += dist;
-        return t - timer;
+    __device__ __forceinline__ uint64_t transmit(int src, int dst, int len, uint64_t timer) {
+        return net_transmit(base, g->off_qhdr, g->off_qring, g->router_delay, g->link_delay, g->inject_delay,
+                            g->header_flits, g->data_width, g->net_width, g->net_type, src, dst, len, timer);
     }
 
     // ------------------------------------------------------------ sets
@@ -515,7 +568,7 @@ struct Engine {
     }
 
     __device__ __forceinline__ int dram() {
-        s_dram++;
+        stat_add(SN_DRAM, 1);
         return g->dram_access_time;
     }
 
@@ -529,7 +582,7 @@ struct Engine {
         set_load(v, at<LineMeta>(L.off_meta), at<int64_t>(L.off_ts), L.nsets, L.nways, L.offbits, L.idxbits,
                  (uint64_t)cid, r.addr);
         if (!rl32(alive_v, cid & 63)) return 0;   // cache never created: NULL in the reference
-        s_lockdown++;
+        stat_add(SN_LOCKDOWN, 1);
         int d = L.access_time;
         int way = set_find(v, L.nways, r.prog);
         if (way >= 0) {
@@ -574,7 +627,7 @@ struct Engine {
     }
     __device__ __forceinline__ bool pool_alloc(uint64_t* idx) {
         if (pool_top <= 0) {
-            s_err |= PU_ERRF_POOL;
+            err_or(PU_ERRF_POOL);
             stop = true;
             return false;
         }
@@ -594,7 +647,7 @@ struct Engine {
         } else if (nsh > 0) {
             return (int)(sh & 0xFFFF);
         }
-        s_err |= PU_ERRF_EMPTY_SHARER;     // *sharer_set.begin() on an empty set
+        err_or(PU_ERRF_EMPTY_SHARER);     // *sharer_set.begin() on an empty set
         return 0;
     }
     __device__ int count_sharers(uint32_t nsh, uint64_t sh) const {
@@ -676,7 +729,7 @@ struct Engine {
     __device__ int broadcast(int home, const Req& r, int64_t base_t) {
         constexpr int last = NL - 1;
         int pipe = 0, mx = 0;
-        s_bcast++;
+        stat_add(SN_BCAST, 1);
         for (int i = 0; i < g->num_cores; i++) {
             int t = pipe;
             t += (int)transmit(home, i, 0, (uint64_t)(base_t + t));
@@ -764,7 +817,7 @@ struct Engine {
             sh = (uint64_t)cid;
             delay += dram();
         } else if (way < 0) {
-            s_err |= PU_ERRF_WB_MISS;         // WB missed at home: NULL deref in the reference (Q13)
+            err_or(PU_ERRF_WB_MISS);         // WB missed at home: NULL deref in the reference (Q13)
             *out_state = ST_I;
             return delay;
         } else {
@@ -846,10 +899,12 @@ struct Engine {
         set_load(v, meta, tsa, L.nsets, L.nways, L.offbits, L.idxbits, (uint64_t)cid, r.addr);
         mark_alive(LV, cid);
         if (L.has_bus) {              // Bus::access (bus.cpp:55-61)
-            s_busacc++;
-            uint64_t bl = (uint64_t)g->bus_latency;
-            int db = (int)q_op(L.bus_q0 + cid, (uint64_t)(timer + dly), bl, bl);
-            s_bus_cont += (uint64_t)(int64_t)db;
+            stat_add(SN_BUSACC, 1);
+            uint64_t bl = (uint64_t)g->bus_latency, mg1 = 0, err = 0;
+            int db = (int)q_op(net_ctx(), L.bus_q0 + cid, (uint64_t)(timer + dly), bl, bl, mg1, err);
+            stat_add(SN_MG1, mg1);
+            if (err) err_or(err);
+            stat_add(SN_BUSCONT, (uint64_t)(int64_t)db);
             dly += db;
         }
         if (!hit) count(L.off_cnt, cid, 0);
@@ -921,10 +976,10 @@ struct Engine {
     // System::access (system.cpp:144-168), directory system, TLB off.
     __device__ int access(int core, const Req& r, int64_t timer) {
         if (core < 0 || core >= g->num_cores) {
-            s_err |= PU_ERRF_CORE_RANGE;
+            err_or(PU_ERRF_CORE_RANGE);
             return -1;
         }
-        s_reqs++;
+        stat_add(SN_REQS, 1);
         hit = false;
         dly = 0;
         mesi<0>(core, r, timer + dly);
@@ -934,23 +989,30 @@ struct Engine {
     __device__ void flush_stats() {
         if (ln != 0) return;
         EngineStats* S = at<EngineStats>(g->off_stats);
-        atomic_add_u64(&S->net_accesses, s_net_acc);
-        atomic_add_u64(&S->net_distance, s_net_dist);
-        atomic_add_u64(&S->net_total_delay, s_net_total);
-        atomic_add_u64(&S->net_router_delay, s_net_router);
-        atomic_add_u64(&S->net_link_delay, s_net_link);
-        atomic_add_u64(&S->net_inject_delay, s_net_inject);
-        atomic_add_u64(&S->dram_accesses, s_dram);
-        atomic_add_u64(&S->total_bus_contention, s_bus_cont);
-        atomic_add_u64(reinterpret_cast<uint64_t*>(&S->total_num_broadcast), (uint64_t)s_bcast);
-        atomic_add_u64(&S->link_flits, s_flits);
-        atomic_add_u64(&S->mg1_calls, s_mg1);
-        atomic_add_u64(&S->lockdown_calls, s_lockdown);
-        atomic_add_u64(&S->bus_accesses, s_busacc);
-        atomic_add_u64(&S->requests, s_reqs);
-        __hip_atomic_fetch_or(&S->error_flags, s_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomic_add_u64(&S->net_accesses, lds_stat[SN_ACC]);
+        atomic_add_u64(&S->net_distance, lds_stat[SN_DIST]);
+        atomic_add_u64(&S->net_total_delay, lds_stat[SN_TOTAL]);
+        atomic_add_u64(&S->net_router_delay, lds_stat[SN_ROUTER]);
+        atomic_add_u64(&S->net_link_delay, lds_stat[SN_LINK]);
+        atomic_add_u64(&S->net_inject_delay, lds_stat[SN_INJECT]);
+        atomic_add_u64(&S->dram_accesses, lds_stat[SN_DRAM]);
+        atomic_add_u64(&S->total_bus_contention, lds_stat[SN_BUSCONT]);
+        atomic_add_u64(reinterpret_cast<uint64_t*>(&S->total_num_broadcast), lds_stat[SN_BCAST]);
+        atomic_add_u64(&S->link_flits, lds_stat[SN_FLITS]);
+        atomic_add_u64(&S->mg1_calls, lds_stat[SN_MG1]);
+        atomic_add_u64(&S->lockdown_calls, lds_stat[SN_LOCKDOWN]);
+        atomic_add_u64(&S->bus_accesses, lds_stat[SN_BUSACC]);
+        atomic_add_u64(&S->requests, lds_stat[SN_REQS]);
+        __hip_atomic_fetch_or(&S->error_flags, (uint64_t)lds_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 };
+
+__device__ __forceinline__ void stats_init() {
+    const int ln = lane_id();
+    if (ln < SN_COUNT) lds_stat[ln] = 0;
+    if (ln == 0) lds_err = 0;
+    __syncthreads();
+}
 
 // One workgroup (= one wavefront) per replica.  Replica replica0 + blockIdx.x
 // processes reqs[off[blockIdx.x] .. off[blockIdx.x+1]) in order: the message
@@ -965,9 +1027,7 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
     e.g = g;
     e.ln = lane_id();
     e.base = arena + (size_t)(replica0 + (int)blockIdx.x) * g->replica_bytes;
-    e.s_net_acc = e.s_net_dist = e.s_net_total = e.s_net_router = e.s_net_link = e.s_net_inject = 0;
-    e.s_dram = e.s_bus_cont = e.s_flits = e.s_mg1 = e.s_lockdown = e.s_busacc = e.s_reqs = e.s_err = 0;
-    e.s_bcast = 0;
+    stats_init();
     e.dly = 0;
     e.hit = false;
 
@@ -996,7 +1056,7 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
         done++;
         D += d - 1;
         if (D < 0) {                        // prime.cpp:130-134
-            e.s_err |= PU_ERRF_NEG_DELAY;
+            err_or(PU_ERRF_NEG_DELAY);
             halted = 1;
         }
         if (e.stop) halted = 1;            // engine limit hit (sharer pool): cannot continue exactly
@@ -1007,6 +1067,7 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
         rs->processed += done;
         rs->pool_top = e.pool_top;
     }
+    __syncthreads();
     e.flush_stats();
 }
 
@@ -1039,15 +1100,15 @@ __global__ __launch_bounds__(64) void unit_queue_kernel(const Geo* __restrict__ 
     e.g = g;
     e.ln = lane_id();
     e.base = base;
-    e.s_mg1 = 0;
-    e.s_err = 0;
     e.pool_top = 0;
     e.stop = false;
+    const NetCtx c = e.net_ctx();
+    uint64_t calls = 0, err = 0;
     for (uint64_t i = 0; i < n; i++) {
-        uint64_t d = e.q_op(0, t[i], p[i], minp);
+        uint64_t d = q_op(c, 0, t[i], p[i], minp, calls, err);
         if (e.ln == 0) out[i] = d;
     }
-    if (e.ln == 0) *mg1 = e.s_mg1;
+    if (e.ln == 0) *mg1 = calls;
 }
 
 __global__ __launch_bounds__(64) void unit_network_kernel(const Geo* __restrict__ g, char* base,
@@ -1060,15 +1121,14 @@ __global__ __launch_bounds__(64) void unit_network_kernel(const Geo* __restrict_
     e.g = g;
     e.ln = lane_id();
     e.base = base;
-    e.s_net_acc = e.s_net_dist = e.s_net_total = e.s_net_router = e.s_net_link = e.s_net_inject = 0;
-    e.s_dram = e.s_bus_cont = e.s_flits = e.s_mg1 = e.s_lockdown = e.s_busacc = e.s_reqs = e.s_err = 0;
-    e.s_bcast = 0;
+    stats_init();
     e.pool_top = 0;
     e.stop = false;
     for (uint64_t i = 0; i < n; i++) {
         uint64_t d = e.transmit(src[i], dst[i], len[i], timer[i]);
         if (e.ln == 0) out[i] = d;
     }
+    __syncthreads();
     e.flush_stats();
 }
 
