@@ -99,6 +99,9 @@ def main() -> None:
     ap.add_argument("--chunk", type=int, default=2500, help="requests per replica per step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) normally; gloo for CPU-side rehearsal")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC traffic summary written by tools/pmc_traffic.py for this kernel")
     args = ap.parse_args()
 
     import torch
@@ -113,7 +116,9 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(args.dist_backend, init_method="env://")
+    # PU_BENCH_DEVICE pins every rank to one card (rehearsing N>1 on a 1-GPU box)
+    local = int(os.environ.get("PU_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -196,13 +201,24 @@ def main() -> None:
     # went negative stops there, like the reference's handler (prime.cpp:130-134)
     processed = int(delta["requests"])
     halted = sum(1 for r in range(R) if um.stats(r).error_flags & A.PU_ERRF_NEG_DELAY)
-    t_max, tot_processed = reduce_run(elapsed, processed, dev)
+    t_max, tot_processed = reduce_run(elapsed, processed, dev if args.dist_backend == "nccl" else None)
     value = tot_processed / t_max
 
     # ---- roofline of the engine kernel (per launch, this rank)
     avg_ms = float(np.mean(kern_ms))
     bytes_per_launch = alg_bytes(delta, cfg) / args.steps
     achieved = bytes_per_launch / (avg_ms / 1e3) / 1e9
+
+    # HBM traffic from the PMC counters (FETCH_SIZE + WRITE_SIZE, separate rocprofv3
+    # passes of this same command, tools/pmc_traffic.py): bytes per access x this
+    # launch's accesses
+    traffic, traffic_src = None, None
+    if os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        traffic = tj["hbm_bytes_per_access"] * (processed / args.steps)
+        traffic_src = (f"{os.path.relpath(args.traffic_json, ROOT)}: {tj['hbm_bytes_per_access']:.0f} B/access "
+                       f"measured at {tj['replicas']} replicas x {tj['requests_per_replica_per_launch']} requests")
 
     result = None
     if rank == 0:
@@ -251,7 +267,8 @@ def main() -> None:
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": "uncore_kernel<1>",
                 "avg_launch_ms": avg_ms,
                 "alg_bytes_per_launch": bytes_per_launch,

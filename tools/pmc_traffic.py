@@ -1,0 +1,119 @@
+"""Collect the engine kernel's HBM traffic from PMC counters (run on the GPU box).
+
+Follows MI355X_MICROARCH.md §HBM / cdna_hip_programming.md §7: FETCH_SIZE and
+WRITE_SIZE (KB, derived from the TCC EA request counters) are collected in
+SEPARATE rocprofv3 passes (FETCH_SIZE needs 3 TCC slots, WRITE_SIZE 2), each
+with nothing but the counter pass; plus one --kernel-trace --stats pass for
+durations.  Per launch of uncore_kernel: bytes = (FETCH_SIZE + WRITE_SIZE) *
+1024.  gfx950 reports FETCH_SIZE at exactly 1/2 for wide coalesced 16-B/lane
+streaming reads; this kernel's reads are 8-40 B per lane gathers, for which the
+guide gives no calibration, so the raw figure is reported next to a 2x-read
+upper bound and both are labelled.
+
+    python tools/pmc_traffic.py --out profiles/r1_traffic.json -- --steps 3 --warmup 1 --no-cpu
+
+Writes the summary JSON, and copies the rocprofv3 summaries under profiles/.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = "uncore_kernel"
+
+
+def run(cmd, log):
+    print("+", " ".join(cmd), flush=True)
+    with open(log, "w") as f:
+        r = subprocess.run(cmd, cwd=ROOT, stdout=f, stderr=subprocess.STDOUT, timeout=900)
+    if r.returncode != 0:
+        raise SystemExit(f"{cmd[0]} failed ({r.returncode}); see {log}")
+
+
+def counter_rows(d):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    with open(files[0]) as f:
+        return list(csv.DictReader(f))
+
+
+def per_dispatch(rows, counter):
+    vals = {}
+    for r in rows:
+        if KERNEL in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
+            did = int(r["Dispatch_Id"])
+            vals[did] = vals.get(did, 0.0) + float(r["Counter_Value"])
+    return [vals[k] for k in sorted(vals)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--work", default=os.path.join(ROOT, "gpurun_out", "pmc"))
+    ap.add_argument("bench_args", nargs=argparse.REMAINDER)
+    a = ap.parse_args()
+    bargs = [x for x in a.bench_args if x != "--"]
+    os.makedirs(a.work, exist_ok=True)
+    os.environ.setdefault("TMPDIR", "/tmp")
+    py = sys.executable
+    bench = [py, os.path.join(ROOT, "bench.py"), *bargs]
+    passes = {}
+    for name, extra in (("fetch", ["--pmc", "FETCH_SIZE"]), ("write", ["--pmc", "WRITE_SIZE"]),
+                        ("trace", ["--kernel-trace", "--stats"])):
+        d = os.path.join(a.work, name)
+        shutil.rmtree(d, ignore_errors=True)
+        run(["rocprofv3", *extra, "--output-format", "csv", "-d", d, "-o", "run", "--", *bench],
+            os.path.join(a.work, f"{name}.log"))
+        passes[name] = d
+    with open(os.path.join(a.work, "trace.log")) as f:
+        bench_line = json.loads([ln for ln in f if ln.startswith("{")][-1])
+    fetch = per_dispatch(counter_rows(passes["fetch"]), "FETCH_SIZE")
+    write = per_dispatch(counter_rows(passes["write"]), "WRITE_SIZE")
+    steps, warm = bench_line["steps"], bench_line["warmup"]
+    n = min(len(fetch), len(write))
+    timed = list(range(n - steps, n))             # the timed launches are the last `steps`
+    f_kb = sum(fetch[i] for i in timed) / steps
+    w_kb = sum(write[i] for i in timed) / steps
+    R = bench_line["config"]["replicas_per_gpu"]
+    chunk = bench_line["config"]["requests_per_replica_per_step"]
+    accesses = R * chunk
+    raw = (f_kb + w_kb) * 1024.0
+    upper = (2.0 * f_kb + w_kb) * 1024.0
+    out = {
+        "kernel": KERNEL,
+        "launches_measured": steps,
+        "warmup": warm,
+        "replicas": R,
+        "requests_per_replica_per_launch": chunk,
+        "fetch_size_kb_per_launch": f_kb,
+        "write_size_kb_per_launch": w_kb,
+        "hbm_bytes_per_launch": raw,
+        "hbm_bytes_per_launch_read_x2_bound": upper,
+        "hbm_bytes_per_access": raw / accesses,
+        "alg_bytes_per_launch": bench_line["roofline"]["alg_bytes_per_launch"],
+        "alg_bytes_per_access": bench_line["roofline"]["alg_bytes_per_launch"] / accesses,
+        "avg_launch_ms_under_profiler": bench_line["roofline"]["avg_launch_ms"],
+        "note": "FETCH_SIZE+WRITE_SIZE (KB) x 1024 per timed launch, separate --pmc passes; gfx950 halves "
+                "FETCH_SIZE for 16-B/lane streaming reads (MI355X_MICROARCH.md §HBM), uncalibrated for this "
+                "kernel's 8-40 B gathers, hence the x2-read bound",
+        "bench_args": bargs,
+    }
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+    prefix = os.path.splitext(a.out)[0]
+    for name in ("fetch", "write", "trace"):
+        for src in glob.glob(os.path.join(passes[name], "**", "*stats.csv"), recursive=True):
+            shutil.copy(src, f"{prefix}_{name}_{os.path.basename(src)}")
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
