@@ -46,6 +46,9 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
     uint32_t hi = rl32((uint32_t)(v >> 32), l);
     return ((uint64_t)hi << 32) | lo;
 }
+// lane l of v becomes x (x wave-uniform)
+__device__ __forceinline__ uint32_t wl32(uint32_t v, uint32_t x, int l) { return (int)threadIdx.x == l ? x : v; }
+__device__ __forceinline__ uint64_t wl64(uint64_t v, uint64_t x, int l) { return (int)threadIdx.x == l ? x : v; }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ uint32_t uni32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
@@ -103,6 +106,7 @@ struct RouteView {
 };
 
 #define AS1 __attribute__((address_space(1)))
+#define PU_RING_PF 8   // staged rings in flight per wave (16 KB LDS)
 // native vectors (not classes), so loads/stores through global-address-space
 // pointers need no conversion: slot = {first, second}, header = 10 dwords
 typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
@@ -138,6 +142,27 @@ __device__ __forceinline__ AS1 v2u64* q_ring(const NetCtx& c, int q) {
 }
 __device__ __forceinline__ AS1 uint32_t* q_hdr(const NetCtx& c, int q) {
     return reinterpret_cast<AS1 uint32_t*>(c.base + c.off_qhdr + (uint64_t)q * sizeof(QueueHdr));
+}
+
+// Load the `cnt` live slots of ring q starting at `head` (lane l holds slots l
+// and l+64); dead slots are not fetched and read as 0.
+__device__ __forceinline__ void ring_load(const NetCtx& c, int q, uint32_t head, uint32_t cnt, RingView& v) {
+    const AS1 v2u64* R = q_ring(c, q);
+    const int ln = lane_id();
+    v = RingView{0, 0, 0, 0};
+    if ((((uint32_t)ln - head) & (PU_QRING - 1)) < cnt) {
+        v2u64 a = R[ln];
+        v.lf = a.x;
+        v.ls = a.y;
+    }
+    if ((((uint32_t)ln + 64 - head) & (PU_QRING - 1)) < cnt) {
+        v2u64 b = R[ln + 64];
+        v.hf = b.x;
+        v.hs = b.y;
+    }
+    // settle the loads here: otherwise hipcc carries them as pending into code
+    // shared with the LDS-staged path and drains every staging DMA there
+    asm volatile("" : "+v"(v.lf), "+v"(v.ls), "+v"(v.hf), "+v"(v.hs));
 }
 
 // M/G/1 (queue_model_m_g_1.cpp:16-42), reference operation order.
@@ -216,38 +241,55 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
     if (op == 1 || op == 2) {
         if (jl == k) { if (op == 1) ls = t; else lf = nf; dl = true; }
         if (jh == k) { if (op == 1) hs = t; else hf = nf; dh = true; }
-    } else if (op == 3) {
-        if (k == 0) {
-            head = (head + 1) & (PU_QRING - 1);
-        } else {
-            // logical [k+1, cnt) move down one: slot s takes slot s+1
-            const int src = (ln + 1) & 63;
-            uint64_t a_f = shfl64(v.lf, src), a_s = shfl64(v.ls, src);
-            uint64_t b_f = shfl64(v.hf, src), b_s = shfl64(v.hs, src);
-            uint64_t sl_f = ln == 63 ? b_f : a_f, sl_s = ln == 63 ? b_s : a_s;
-            uint64_t sh_f = ln == 63 ? a_f : b_f, sh_s = ln == 63 ? a_s : b_s;
-            if (jl >= k && jl + 1 < cnt) { lf = sl_f; ls = sl_s; dl = true; }
-            if (jh >= k && jh + 1 < cnt) { hf = sh_f; hs = sh_s; dh = true; }
-        }
+    } else if (op == 3 && k == 0) {
+        head = (head + 1) & (PU_QRING - 1);
         cnt = cnt - 1;
-    } else {  // split: node k keeps [first, t]; [t+p, second] inserted at k+1
-        const int src = (ln + 63) & 63;
+    } else {
+        // remove node k (3) or split it (4): the logical order is all that
+        // matters, so move whichever side of node k is shorter (the prefix
+        // moves by shifting `head`) — half the slot rewrites on average.
+        const bool split = op == 4;
+        const bool prefix = split ? (2 * k + 1 < cnt) : (k < cnt - 1 - k);
+        const int dir = (split != prefix) ? -1 : 1;     // slot takes slot+dir
+        const int src = (ln + dir) & 63;
+        const int wrap = dir > 0 ? 63 : 0;
         uint64_t a_f = shfl64(v.lf, src), a_s = shfl64(v.ls, src);
         uint64_t b_f = shfl64(v.hf, src), b_s = shfl64(v.hs, src);
-        uint64_t pl_f = ln == 0 ? b_f : a_f, pl_s = ln == 0 ? b_s : a_s;
-        uint64_t ph_f = ln == 0 ? a_f : b_f, ph_s = ln == 0 ? a_s : b_s;
-        if (jl == k) { ls = t; dl = true; }
-        else if (jl == k + 1) { lf = tp; ls = s; dl = true; }
-        else if (jl >= k + 2 && jl <= cnt) { lf = pl_f; ls = pl_s; dl = true; }
-        if (jh == k) { hs = t; dh = true; }
-        else if (jh == k + 1) { hf = tp; hs = s; dh = true; }
-        else if (jh >= k + 2 && jh <= cnt) { hf = ph_f; hs = ph_s; dh = true; }
-        cnt = cnt + 1;
+        const uint64_t sl_f = ln == wrap ? b_f : a_f, sl_s = ln == wrap ? b_s : a_s;
+        const uint64_t sh_f = ln == wrap ? a_f : b_f, sh_s = ln == wrap ? a_s : b_s;
+        auto edit = [&](uint32_t j, uint64_t& xf, uint64_t& xs, uint64_t mf, uint64_t ms) -> bool {
+            if (!split) {
+                if (prefix ? (j >= 1 && j <= k) : (j >= k && j + 1 < cnt)) { xf = mf; xs = ms; return true; }
+            } else if (!prefix) {      // node k keeps [first, t]; [t+p, second] at k+1; tail moves up
+                if (j == k) { xs = t; return true; }
+                if (j == k + 1) { xf = tp; xs = s; return true; }
+                if (j >= k + 2 && j <= cnt) { xf = mf; xs = ms; return true; }
+            } else {                   // head moves back one; nodes [0, k) move down
+                const uint32_t jn = (j + 1) & (PU_QRING - 1);
+                if (jn < k) { xf = mf; xs = ms; return true; }
+                if (jn == k) { xf = f; xs = t; return true; }
+                if (jn == k + 1) { xf = tp; xs = s; return true; }
+            }
+            return false;
+        };
+        dl = edit(jl, lf, ls, sl_f, sl_s);
+        dh = edit(jh, hf, hs, sh_f, sh_s);
+        if (prefix) head = (head + (split ? PU_QRING - 1 : 1)) & (PU_QRING - 1);
+        cnt = split ? cnt + 1 : cnt - 1;
     }
     AS1 v2u64* R = q_ring(c, q);
     if (dl) R[ln] = v2u64{lf, ls};
     if (dh) R[ln + 64] = v2u64{hf, hs};
     return d;
+}
+
+// Header write-back of queue q by the calling lane(s).
+__device__ __forceinline__ void q_store_hdr(const NetCtx& c, int q, const QState& st) {
+    AS1 uint32_t* H = q_hdr(c, q);
+    uint64_t sb = (uint64_t)__double_as_longlong(st.sum), qb = (uint64_t)__double_as_longlong(st.sum_sq);
+    *reinterpret_cast<AS1 v4u32*>(H) = v4u32{st.head, st.count, (uint32_t)st.n, (uint32_t)(st.n >> 32)};
+    *reinterpret_cast<AS1 v4u32*>(H + 4) = v4u32{(uint32_t)sb, (uint32_t)(sb >> 32), (uint32_t)qb, (uint32_t)(qb >> 32)};
+    *reinterpret_cast<AS1 v2u32*>(H + 8) = v2u32{(uint32_t)st.newest, (uint32_t)(st.newest >> 32)};
 }
 
 // M/G/1 update (queue_model_m_g_1.cpp:45-55) and header write-back (lane 0).
@@ -257,14 +299,7 @@ __device__ __forceinline__ void q_finish(const NetCtx& c, int q, QState& st, uin
     st.n = st.n + 1;
     uint64_t fin = t + d + p;
     st.newest = fin > st.newest ? fin : st.newest;
-    if (lane_id() == 0) {
-        AS1 uint32_t* H = q_hdr(c, q);
-        uint64_t sb = (uint64_t)__double_as_longlong(st.sum), qb = (uint64_t)__double_as_longlong(st.sum_sq);
-        *reinterpret_cast<AS1 v4u32*>(H) = v4u32{st.head, st.count, (uint32_t)st.n, (uint32_t)(st.n >> 32)};
-        *reinterpret_cast<AS1 v4u32*>(H + 4) =
-            v4u32{(uint32_t)sb, (uint32_t)(sb >> 32), (uint32_t)qb, (uint32_t)(qb >> 32)};
-        *reinterpret_cast<AS1 v2u32*>(H + 8) = v2u32{(uint32_t)st.newest, (uint32_t)(st.newest >> 32)};
-    }
+    if (lane_id() == 0) q_store_hdr(c, q, st);
 }
 
 // One computeQueueDelay given the header and the first two interval starts.
@@ -281,10 +316,8 @@ __device__ __forceinline__ uint64_t q_step(const NetCtx& c, int q, QState& st, u
         d = mg1_wait(st);
         mg1++;
     } else {
-        const AS1 v2u64* R = q_ring(c, q);
-        const int ln = lane_id();
-        v2u64 a = R[ln], b = R[ln + 64];
-        RingView v{a.x, a.y, b.x, b.y};
+        RingView v;
+        ring_load(c, q, st.head, st.count, v);
         d = tree_op(c, q, v, st.head, st.count, t, p, minp, err);
     }
     q_finish(c, q, st, t, p, d);
@@ -370,6 +403,66 @@ __device__ __forceinline__ int net_route_link(const NetCtx& c, int h, int sx, in
     return net_link(c, rx, ry, z, u ? 4 : 5);
 }
 
+// LDS staging ring for predicted tree hops: PU_RING_PF full link rings per wave
+// (one wave per workgroup), filled by global_load_lds_dwordx4 and consumed in
+// hop order behind a counted vmcnt (loads, stores and LDS-DMA retire in issue
+// order, MI355X_MICROARCH.md §waitcnt; hipcc would drain everything instead).
+static __shared__ v2u64 lds_ring[PU_RING_PF][PU_QRING];
+
+// Stage ring q (live slots [head, head+cnt)) into LDS slot `slot`; dead slots
+// read the head slot instead (one shared line) and are never used.
+__device__ __forceinline__ void ring_dma(const NetCtx& c, int q, uint32_t head, uint32_t cnt, int slot) {
+    const int ln = lane_id();
+    const AS1 v2u64* R = q_ring(c, q);
+    const AS1 v2u64* ga = R + ((((uint32_t)ln - head) & (PU_QRING - 1)) < cnt ? (uint32_t)ln : head);
+    const AS1 v2u64* gb = R + ((((uint32_t)ln + 64 - head) & (PU_QRING - 1)) < cnt ? (uint32_t)ln + 64 : head);
+    const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) v2u64*)&lds_ring[slot][0];
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(la), hi = lo + 64 * sizeof(v2u64);
+    unsigned keep;
+    // lgkmcnt(0): the slot's previous ds_reads have returned before it is refilled
+    asm volatile(
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(ga), "v"(gb), "s"(lo), "s"(hi)
+        : "memory");
+}
+// Stage the ring of window hop jj (its header is in lanes of hhead/hcnt).
+__device__ __forceinline__ void ring_dma_hop(const NetCtx& c, int rq, uint32_t hhead, uint32_t hcnt, int jj,
+                                             int slot) {
+    uint32_t head = rl32(hhead, jj), cnt = rl32(hcnt, jj);
+    if (cnt >= PU_QMAX) {           // the prune this hop will do first
+        head = (head + 1) & (PU_QRING - 1);
+        cnt--;
+    }
+    ring_dma(c, (int)rl32((uint32_t)rq, jj), head, cnt, slot);
+}
+// Wait until at most `n` newer staging rings (2 DMAs each) are still in flight.
+__device__ __forceinline__ void vm_wait_dma(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    }
+}
+__device__ __forceinline__ void ring_from_lds(int slot, RingView& v) {
+    const int ln = lane_id();
+    const v2u64 a = lds_ring[slot][ln], b = lds_ring[slot][ln + 64];
+    v = RingView{a.x, a.y, b.x, b.y};
+}
+
 // Network::transmit (network.cpp:97-160).  Out of line (one copy), every
 // argument made wave-uniform so the hop loop runs on SGPRs and scalar branches.
 // Lane h prefetches hop h's link header and the two interval starts at its
@@ -420,14 +513,86 @@ __device__ __noinline__ uint64_t net_transmit(char* base_in, uint64_t off_qhdr, 
             rf1 = R[(ha.x + 1) & (PU_QRING - 1)].x;
         }
         const int nh = hops - b0 < 64 ? hops - b0 : 64;
+        // Everything about hop h that does not depend on its arrival time is
+        // computed by lane h here, once per window: the prune (history_tree.cpp:
+        // 49-55), the front interval, the M/G/1 wait from the pre-update moments
+        // (queue_model_m_g_1.cpp:16-42) and the moment updates of q_finish.  The
+        // route's links are distinct, so no hop sees another hop's update.
+        uint32_t vhead = ha.x, vcnt = ha.y;
+        uint64_t vfront = rf0;
+        if (vcnt >= PU_QMAX) {
+            vhead = (vhead + 1) & (PU_QRING - 1);
+            vcnt--;
+            vfront = rf1;
+        }
+        const QState hs = hdr_state(ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w, hc.x, hc.y);
+        const uint64_t vmg1 = ln < nh ? mg1_wait(hs) : 0;
+        uint64_t vfin = 0;              // t + d + p of hop h, filled in by the hop loop
+        // Hop j arrives no earlier than LB_j = t + (j+1)*router + j*link_delay
+        // (queue delays are >= 0).  A hop whose front free interval starts by
+        // LB_j + p cannot take the M/G/1 branch, so its full ring is certainly
+        // needed: stage those rings now, PU_RING_PF ahead, in hop order.
+        bool pred = false;
+        if (ln < nh) {
+            const uint64_t lb = t + (uint64_t)(ln + 1) * c.router + (uint64_t)ln * c.link_delay;
+            pred = vfront <= lb + (uint64_t)plen;
+        }
+        const uint64_t M = ballot(pred);
+        uint64_t mi = M, mc = M;        // issue / consume cursors over the predicted hops
+        int issued = 0, consumed = 0;
+        while (mi && issued < PU_RING_PF) {
+            const int jj = (int)__builtin_ctzll(mi);
+            mi &= mi - 1;
+            ring_dma(c, (int)rl32((uint32_t)rq, jj), rl32(vhead, jj), rl32(vcnt, jj), issued % PU_RING_PF);
+            issued++;
+        }
+        // ---- the arrival-time recurrence, hop by hop
         for (int j = 0; j < nh; j++) {
             t += c.router;
-            const int q = (int)rl32((uint32_t)rq, j);
-            QState st = hdr_state(rl32(ha.x, j), rl32(ha.y, j), rl32(ha.z, j), rl32(ha.w, j), rl32(hb.x, j),
-                                  rl32(hb.y, j), rl32(hb.z, j), rl32(hb.w, j), rl32(hc.x, j), rl32(hc.y, j));
-            t += q_step(c, q, st, rl64(rf0, j), rl64(rf1, j), t, (uint64_t)plen, c.link_delay, mg1, err) +
-                 c.link_delay;
+            uint64_t d;
+            if (rl64(vfront, j) > t + (uint64_t)plen) {   // older than the tracked history: M/G/1
+                d = rl64(vmg1, j);
+                mg1++;
+            } else {
+                const int q = (int)rl32((uint32_t)rq, j);
+                uint32_t head = rl32(vhead, j), cnt = rl32(vcnt, j);
+                RingView v;
+                if (mc && j == (int)__builtin_ctzll(mc)) {
+                    // predicted: its ring is (being) staged in LDS slot consumed % PF
+                    mc &= mc - 1;
+                    vm_wait_dma(issued - consumed - 1);
+                    ring_from_lds(consumed % PU_RING_PF, v);
+                    consumed++;
+                    d = tree_op(c, q, v, head, cnt, t, (uint64_t)plen, c.link_delay, err);
+                    if (mi) {                   // keep PF rings in flight
+                        const int jj = (int)__builtin_ctzll(mi);
+                        mi &= mi - 1;
+                        ring_dma(c, (int)rl32((uint32_t)rq, jj), rl32(vhead, jj), rl32(vcnt, jj),
+                                 issued % PU_RING_PF);
+                        issued++;
+                    }
+                } else {                        // not predicted (arrival pushed past the front)
+                    ring_load(c, q, head, cnt, v);
+                    d = tree_op(c, q, v, head, cnt, t, (uint64_t)plen, c.link_delay, err);
+                }
+                vhead = wl32(vhead, head, j);
+                vcnt = wl32(vcnt, cnt, j);
+            }
+            vfin = wl64(vfin, t + d + (uint64_t)plen, j);
+            t += d + c.link_delay;
         }
+        // ---- header write-back, one hop per lane (queue_model_m_g_1.cpp:45-55)
+        if (ln < nh) {
+            QState st = hs;
+            st.head = vhead;
+            st.count = vcnt;
+            st.sum_sq = st.sum_sq + (double)plen * (double)plen;
+            st.sum = st.sum + (double)plen;
+            st.n = st.n + 1;
+            st.newest = vfin > st.newest ? vfin : st.newest;
+            q_store_hdr(c, rq, st);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no staging DMA outlives its window
     }
     t += c.router;
     t += (uint64_t)(plen - 1);
