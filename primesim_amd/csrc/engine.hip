@@ -129,6 +129,27 @@ __device__ __forceinline__ void err_or(uint64_t f) {
     if (lane_id() == 0) atomicOr(&lds_err, (unsigned long long)f);
 }
 
+// Region cycle counters, compiled in only with -DPU_PROF (the profiling build,
+// libprimeuncore_prof.so; tools/prof_regions.py).  Regions are inclusive.
+enum ProfId {
+    PF_LOOP, PF_REQ, PF_NET, PF_NSETUP, PF_NHOPS, PF_NTREE, PF_NWAIT, PF_NWB, PF_SETL0, PF_SETLN, PF_HOME_LD,
+    PF_HOME, PF_DOWN, PF_WINDOWS, PF_TREEHOPS, PF_DEMAND, PF_T_LDS, PF_T_SEARCH, PF_T_DECIDE, PF_T_EDIT,
+    PF_T_STORE, PF_T_REFILL, PF_COUNT
+};
+#ifdef PU_PROF
+static __shared__ unsigned long long lds_prof[PF_COUNT];
+__device__ unsigned long long g_prof[PF_COUNT];
+#define PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(id, t0) \
+    do { if (lane_id() == 0) atomicAdd(&lds_prof[id], (unsigned long long)(__builtin_amdgcn_s_memtime() - (t0))); } while (0)
+#define PROF_CNT(id, n) \
+    do { if (lane_id() == 0) atomicAdd(&lds_prof[id], (unsigned long long)(n)); } while (0)
+#else
+#define PROF_T(v)
+#define PROF_ADD(id, t0) do { } while (0)
+#define PROF_CNT(id, n) do { } while (0)
+#endif
+
 // Wave-uniform context of the queue/network code (all values in SGPRs).
 struct NetCtx {
     AS1 char* base;            // replica arena
@@ -182,104 +203,145 @@ __device__ __forceinline__ uint64_t mg1_wait(const QState& s) {
     return (uint64_t)ceil(w);
 }
 
+// Whole-wave rotates (DPP): lane i receives lane (i+1)&63 / (i-1)&63.
+__device__ __forceinline__ uint32_t dpp_next(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x134, 0xF, 0xF, false);   // wave_rol:1
+}
+__device__ __forceinline__ uint32_t dpp_prev(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x13C, 0xF, 0xF, false);   // wave_ror:1
+}
+// The 128-slot ring moved by one slot: slot i receives slot i+1 (NEXT) or
+// i-1 (PREV); lane 63 / lane 0 cross between the low and high halves.
+template <bool NEXT>
+__device__ __forceinline__ void ring_shift(uint64_t lo, uint64_t hi, uint64_t& olo, uint64_t& ohi) {
+    const bool cross = NEXT ? lane_id() == 63 : lane_id() == 0;
+    const uint32_t a0 = NEXT ? dpp_next((uint32_t)lo) : dpp_prev((uint32_t)lo);
+    const uint32_t a1 = NEXT ? dpp_next((uint32_t)(lo >> 32)) : dpp_prev((uint32_t)(lo >> 32));
+    const uint32_t b0 = NEXT ? dpp_next((uint32_t)hi) : dpp_prev((uint32_t)hi);
+    const uint32_t b1 = NEXT ? dpp_next((uint32_t)(hi >> 32)) : dpp_prev((uint32_t)(hi >> 32));
+    olo = cross ? (((uint64_t)b1 << 32) | b0) : (((uint64_t)a1 << 32) | a0);
+    ohi = cross ? (((uint64_t)a1 << 32) | a0) : (((uint64_t)b1 << 32) | b0);
+}
+
+// computeQueueDelay's outcome for interval [f, s] if the search stops there
+// (queue_model_history_tree.cpp:74-106): op 1 second<-t, 2 first<-t+d+p,
+// 3 remove, 4 split; returns the delay d.
+__device__ __forceinline__ uint64_t tree_case(uint64_t f, uint64_t s, uint64_t t, uint64_t p, uint64_t minp,
+                                              uint32_t& op) {
+    const uint64_t tp = t + p;
+    const bool ge = t >= f;
+    const bool fit_after = s - tp >= minp;
+    const uint32_t op_ge = (t - f >= minp) ? (fit_after ? 4u : 1u) : (fit_after ? 2u : 3u);
+    const uint32_t op_lt = (s - (f + p) >= minp) ? 2u : 3u;
+    op = ge ? op_ge : op_lt;
+    return ge ? 0 : f - t;
+}
+
 // Tree branch of QueueModelHistoryTree::computeQueueDelay
-// (queue_model_history_tree.cpp:64-112) on the full ring.  head/cnt are the
-// post-prune values and are updated; edited slots are written back.
+// (queue_model_history_tree.cpp:64-112) on the full ring, branch-light: every
+// lane evaluates the search predicate and the outcome for its two slots, the
+// leftmost hit in ring order from `head` is picked with one 128-bit scan, and
+// the edit is one range move (DPP rotate) plus at most two overridden fields.
+// head/cnt are the post-prune values and are updated; edited slots are
+// written back.  The ring side that moves is the shorter one (a prefix move
+// shifts `head`): only the logical order is observable.
 __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingView& v, uint32_t& head,
                                             uint32_t& cnt, uint64_t t, uint64_t p, uint64_t minp, uint64_t& err) {
     const int ln = lane_id();
+    PROF_T(p_s);
     const uint64_t tp = t + p;
     const uint32_t jl = ((uint32_t)ln - head) & (PU_QRING - 1);
     const uint32_t jh = ((uint32_t)ln + 64 - head) & (PU_QRING - 1);
-    bool pl = jl < cnt && ((v.lf <= t && tp <= v.ls) || (t < v.lf && v.ls - v.lf >= p));
-    bool ph = jh < cnt && ((v.hf <= t && tp <= v.hs) || (t < v.hf && v.hs - v.hf >= p));
+    const bool pl = jl < cnt && ((v.lf <= t && tp <= v.ls) || (t < v.lf && v.ls - v.lf >= p));
+    const bool ph = jh < cnt && ((v.hf <= t && tp <= v.hs) || (t < v.hf && v.hs - v.hf >= p));
+    uint32_t opl, oph;
+    const uint64_t dl_ = tree_case(v.lf, v.ls, t, p, minp, opl);
+    const uint64_t dh_ = tree_case(v.hf, v.hs, t, p, minp, oph);
     uint64_t ml = ballot(pl), mh = ballot(ph);
-    // leftmost interval in logical (ring) order starting at `head`
-    uint32_t slot;
-    if (head < 64) {
-        uint64_t ge = ml & (~0ull << head);
-        if (ge) slot = (uint32_t)__builtin_ctzll(ge);
-        else if (mh) slot = 64 + (uint32_t)__builtin_ctzll(mh);
-        else slot = (uint32_t)__builtin_ctzll(ml);
-    } else {
-        uint64_t ge = mh & (~0ull << (head - 64));
-        if (ge) slot = 64 + (uint32_t)__builtin_ctzll(ge);
-        else if (ml) slot = (uint32_t)__builtin_ctzll(ml);
-        else slot = 64 + (uint32_t)__builtin_ctzll(mh);
+    // logical order: rotate the 128-bit hit mask right by head
+    const uint32_t hsh = head & 63;
+    if (head >= 64) {
+        const uint64_t x = ml;
+        ml = mh;
+        mh = x;
     }
-    if ((ml | mh) == 0) {      // search returned NULL: an assert in the reference
+    const uint64_t rlo = hsh ? (ml >> hsh) | (mh << (64 - hsh)) : ml;
+    const uint64_t rhi = hsh ? (mh >> hsh) | (ml << (64 - hsh)) : mh;
+    uint32_t k;
+    if (rlo) k = (uint32_t)__builtin_ctzll(rlo);
+    else if (rhi) k = 64 + (uint32_t)__builtin_ctzll(rhi);
+    else {                        // search returned NULL: an assert in the reference
         err |= PU_ERRF_QUEUE;
-        slot = head;
+        k = 0;
     }
-    const uint32_t k = (slot - head) & (PU_QRING - 1);
-    const uint64_t f = slot < 64 ? rl64(v.lf, (int)slot) : rl64(v.hf, (int)(slot - 64));
-    const uint64_t s = slot < 64 ? rl64(v.ls, (int)slot) : rl64(v.hs, (int)(slot - 64));
-    uint64_t d;
-    int op;  // 1 second<-t, 2 first<-nf, 3 remove, 4 split
-    uint64_t nf = 0;
-    if (t >= f) {
-        d = 0;
-        if (t - f >= minp) {
-            op = (s - tp >= minp) ? 4 : 1;
-        } else if (s - tp >= minp) {
-            op = 2;
-            nf = tp;
-        } else {
-            op = 3;
+    const uint32_t slot = (head + k) & (PU_QRING - 1);
+    PROF_ADD(PF_T_SEARCH, p_s);
+    PROF_T(p_d);
+    const bool hi_half = slot >= 64;
+    const uint32_t op = rl32(hi_half ? oph : opl, (int)(slot & 63));
+    const uint64_t d = rl64(hi_half ? dh_ : dl_, (int)(slot & 63));
+    // the edit as: slots whose logical index is in [r0, r0+rlen) take their
+    // NEXT/PREV neighbour; then first<-fv at logical fi, second<-t at si
+    uint32_t r0 = 0, rlen = 0, fi = 0xFFFFFFFFu, si = 0xFFFFFFFFu;
+    bool next = true;
+    const uint64_t fv = op == 2 ? tp + d : tp;
+    if (op == 1) {
+        si = k;
+    } else if (op == 2) {
+        fi = k;
+    } else if (op == 3) {
+        if (k == 0) {
+            head = (head + 1) & (PU_QRING - 1);
+        } else if (k < cnt - 1 - k) {             // move [0, k) up one, head+1
+            r0 = 1; rlen = k; next = false;
+            head = (head + 1) & (PU_QRING - 1);
+        } else {                                  // move (k, cnt) down one
+            r0 = k; rlen = cnt - 1 - k; next = true;
         }
-    } else {
-        d = f - t;
-        if (s - (f + p) >= minp) {
-            op = 2;
-            nf = f + p;
-        } else {
-            op = 3;
-        }
-    }
-    bool dl = false, dh = false;
-    uint64_t lf = v.lf, ls = v.ls, hf = v.hf, hs = v.hs;
-    if (op == 1 || op == 2) {
-        if (jl == k) { if (op == 1) ls = t; else lf = nf; dl = true; }
-        if (jh == k) { if (op == 1) hs = t; else hf = nf; dh = true; }
-    } else if (op == 3 && k == 0) {
-        head = (head + 1) & (PU_QRING - 1);
         cnt = cnt - 1;
     } else {
-        // remove node k (3) or split it (4): the logical order is all that
-        // matters, so move whichever side of node k is shorter (the prefix
-        // moves by shifting `head`) — half the slot rewrites on average.
-        const bool split = op == 4;
-        const bool prefix = split ? (2 * k + 1 < cnt) : (k < cnt - 1 - k);
-        const int dir = (split != prefix) ? -1 : 1;     // slot takes slot+dir
-        const int src = (ln + dir) & 63;
-        const int wrap = dir > 0 ? 63 : 0;
-        uint64_t a_f = shfl64(v.lf, src), a_s = shfl64(v.ls, src);
-        uint64_t b_f = shfl64(v.hf, src), b_s = shfl64(v.hs, src);
-        const uint64_t sl_f = ln == wrap ? b_f : a_f, sl_s = ln == wrap ? b_s : a_s;
-        const uint64_t sh_f = ln == wrap ? a_f : b_f, sh_s = ln == wrap ? a_s : b_s;
-        auto edit = [&](uint32_t j, uint64_t& xf, uint64_t& xs, uint64_t mf, uint64_t ms) -> bool {
-            if (!split) {
-                if (prefix ? (j >= 1 && j <= k) : (j >= k && j + 1 < cnt)) { xf = mf; xs = ms; return true; }
-            } else if (!prefix) {      // node k keeps [first, t]; [t+p, second] at k+1; tail moves up
-                if (j == k) { xs = t; return true; }
-                if (j == k + 1) { xf = tp; xs = s; return true; }
-                if (j >= k + 2 && j <= cnt) { xf = mf; xs = ms; return true; }
-            } else {                   // head moves back one; nodes [0, k) move down
-                const uint32_t jn = (j + 1) & (PU_QRING - 1);
-                if (jn < k) { xf = mf; xs = ms; return true; }
-                if (jn == k) { xf = f; xs = t; return true; }
-                if (jn == k + 1) { xf = tp; xs = s; return true; }
-            }
-            return false;
-        };
-        dl = edit(jl, lf, ls, sl_f, sl_s);
-        dh = edit(jh, hf, hs, sh_f, sh_s);
-        if (prefix) head = (head + (split ? PU_QRING - 1 : 1)) & (PU_QRING - 1);
-        cnt = split ? cnt + 1 : cnt - 1;
+        if (2 * k + 1 < cnt) {                    // [0, k] down one, head-1; node k-1 = [f, t], k = [t+p, s]
+            r0 = PU_QRING - 1; rlen = k + 1; next = true;
+            si = (k - 1) & (PU_QRING - 1); fi = k;
+            head = (head + PU_QRING - 1) & (PU_QRING - 1);
+        } else {                                  // (k, cnt) up one; node k = [f, t], k+1 = [t+p, s]
+            r0 = k + 1; rlen = cnt - k; next = false;
+            si = k; fi = k + 1;
+        }
+        cnt = cnt + 1;
     }
+    PROF_ADD(PF_T_DECIDE, p_d);
+    PROF_T(p_e);
+    uint64_t lf = v.lf, ls = v.ls, hf = v.hf, hs = v.hs;
+    bool wl = false, wh = false;
+    if (rlen) {
+        uint64_t nlf, nls, nhf, nhs;
+        if (next) {
+            ring_shift<true>(v.lf, v.hf, nlf, nhf);
+            ring_shift<true>(v.ls, v.hs, nls, nhs);
+        } else {
+            ring_shift<false>(v.lf, v.hf, nlf, nhf);
+            ring_shift<false>(v.ls, v.hs, nls, nhs);
+        }
+        wl = ((jl - r0) & (PU_QRING - 1)) < rlen;
+        wh = ((jh - r0) & (PU_QRING - 1)) < rlen;
+        lf = wl ? nlf : lf;
+        ls = wl ? nls : ls;
+        hf = wh ? nhf : hf;
+        hs = wh ? nhs : hs;
+    }
+    lf = jl == fi ? fv : lf;
+    hf = jh == fi ? fv : hf;
+    ls = jl == si ? t : ls;
+    hs = jh == si ? t : hs;
+    wl = wl || jl == fi || jl == si;
+    wh = wh || jh == fi || jh == si;
+    PROF_ADD(PF_T_EDIT, p_e);
+    PROF_T(p_w);
     AS1 v2u64* R = q_ring(c, q);
-    if (dl) R[ln] = v2u64{lf, ls};
-    if (dh) R[ln + 64] = v2u64{hf, hs};
+    if (wl) R[ln] = v2u64{lf, ls};
+    if (wh) R[ln + 64] = v2u64{hf, hs};
+    PROF_ADD(PF_T_STORE, p_w);
     return d;
 }
 
@@ -496,6 +558,8 @@ __device__ __noinline__ uint64_t net_transmit(char* base_in, uint64_t off_qhdr, 
     uint64_t t = timer + c.inject;
     uint64_t mg1 = 0, err = 0;
     for (int b0 = 0; b0 < hops; b0 += 64) {
+        PROF_T(p_setup);
+        PROF_CNT(PF_WINDOWS, 1);
         // ---- prefetch the window: lane h = hop b0+h
         const int h = b0 + ln;
         int rq = 0;
@@ -546,6 +610,8 @@ __device__ __noinline__ uint64_t net_transmit(char* base_in, uint64_t off_qhdr, 
             ring_dma(c, (int)rl32((uint32_t)rq, jj), rl32(vhead, jj), rl32(vcnt, jj), issued % PU_RING_PF);
             issued++;
         }
+        PROF_ADD(PF_NSETUP, p_setup);
+        PROF_T(p_hops);
         // ---- the arrival-time recurrence, hop by hop
         for (int j = 0; j < nh; j++) {
             t += c.router;
@@ -554,16 +620,21 @@ __device__ __noinline__ uint64_t net_transmit(char* base_in, uint64_t off_qhdr, 
                 d = rl64(vmg1, j);
                 mg1++;
             } else {
+                PROF_T(p_tree);
+                PROF_CNT(PF_TREEHOPS, 1);
                 const int q = (int)rl32((uint32_t)rq, j);
                 uint32_t head = rl32(vhead, j), cnt = rl32(vcnt, j);
                 RingView v;
                 if (mc && j == (int)__builtin_ctzll(mc)) {
                     // predicted: its ring is (being) staged in LDS slot consumed % PF
                     mc &= mc - 1;
+                    PROF_T(p_wait);
                     vm_wait_dma(issued - consumed - 1);
+                    PROF_ADD(PF_NWAIT, p_wait);
                     ring_from_lds(consumed % PU_RING_PF, v);
                     consumed++;
                     d = tree_op(c, q, v, head, cnt, t, (uint64_t)plen, c.link_delay, err);
+                    PROF_T(p_r);
                     if (mi) {                   // keep PF rings in flight
                         const int jj = (int)__builtin_ctzll(mi);
                         mi &= mi - 1;
@@ -571,16 +642,21 @@ __device__ __noinline__ uint64_t net_transmit(char* base_in, uint64_t off_qhdr, 
                                  issued % PU_RING_PF);
                         issued++;
                     }
+                    PROF_ADD(PF_T_REFILL, p_r);
                 } else {                        // not predicted (arrival pushed past the front)
+                    PROF_CNT(PF_DEMAND, 1);
                     ring_load(c, q, head, cnt, v);
                     d = tree_op(c, q, v, head, cnt, t, (uint64_t)plen, c.link_delay, err);
                 }
                 vhead = wl32(vhead, head, j);
                 vcnt = wl32(vcnt, cnt, j);
+                PROF_ADD(PF_NTREE, p_tree);
             }
             vfin = wl64(vfin, t + d + (uint64_t)plen, j);
             t += d + c.link_delay;
         }
+        PROF_ADD(PF_NHOPS, p_hops);
+        PROF_T(p_wb);
         // ---- header write-back, one hop per lane (queue_model_m_g_1.cpp:45-55)
         if (ln < nh) {
             QState st = hs;
@@ -593,6 +669,7 @@ __device__ __noinline__ uint64_t net_transmit(char* base_in, uint64_t off_qhdr, 
             q_store_hdr(c, rq, st);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no staging DMA outlives its window
+        PROF_ADD(PF_NWB, p_wb);
     }
     t += c.router;
     t += (uint64_t)(plen - 1);
@@ -643,8 +720,11 @@ struct Engine {
         return c;
     }
     __device__ __forceinline__ uint64_t transmit(int src, int dst, int len, uint64_t timer) {
-        return net_transmit(base, g->off_qhdr, g->off_qring, g->router_delay, g->link_delay, g->inject_delay,
-                            g->header_flits, g->data_width, g->net_width, g->net_type, src, dst, len, timer);
+        PROF_T(p0);
+        uint64_t d = net_transmit(base, g->off_qhdr, g->off_qring, g->router_delay, g->link_delay, g->inject_delay,
+                                  g->header_flits, g->data_width, g->net_width, g->net_type, src, dst, len, timer);
+        PROF_ADD(PF_NET, p0);
+        return d;
     }
 
     // ------------------------------------------------------------ sets
@@ -741,6 +821,13 @@ struct Engine {
     // System::share / System::inval (system.cpp:488-555); LV is the level of `cid`.
     template <int LV, bool INVAL>
     __device__ int down(int cid, const Req& r) {
+        PROF_T(p0);
+        int d = down_impl<LV, INVAL>(cid, r);
+        PROF_ADD(PF_DOWN, p0);
+        return d;
+    }
+    template <int LV, bool INVAL>
+    __device__ int down_impl(int cid, const Req& r) {
         const LevelGeo& L = g->lv[LV];
         uint32_t alive_v = ln == (cid & 63) ? at<uint32_t>(L.off_alive)[cid] : 0u;
         SetView v;
@@ -911,6 +998,13 @@ struct Engine {
     // The home line is read once (lane w: way w, 32 B) and written once at the
     // end: nothing reached from here touches directory lines.
     __device__ int access_home(int cid, int home, const Req& r, int64_t timer, uint32_t* out_state) {
+        PROF_T(p0);
+        int d = access_home_impl(cid, home, r, timer, out_state);
+        PROF_ADD(PF_HOME, p0);
+        return d;
+    }
+    __device__ int access_home_impl(int cid, int home, const Req& r, int64_t timer, uint32_t* out_state) {
+        PROF_T(p_ld);
         const DirGeo& D = g->dir;
         const bool shared = g->shared_llc != 0;
         constexpr int last = NL - 1;
@@ -929,6 +1023,7 @@ struct Engine {
         }
         const uint64_t hm = ballot(mine && m.state != ST_I && m.id == r.prog && m.tag == tag);
         int way = hm ? (int)__builtin_ctzll(hm) : -1;
+        PROF_ADD(PF_HOME_LD, p_ld);
         count(D.off_cnt, home, 0);
         int delay = D.access_time;
         uint32_t st, nsh;
@@ -1061,6 +1156,7 @@ struct Engine {
         LineMeta* meta = at<LineMeta>(L.off_meta);
         int64_t* tsa = at<int64_t>(L.off_ts);
         SetView v;
+        PROF_T(p_set);
         set_load(v, meta, tsa, L.nsets, L.nways, L.offbits, L.idxbits, (uint64_t)cid, r.addr);
         mark_alive(LV, cid);
         if (L.has_bus) {              // Bus::access (bus.cpp:55-61)
@@ -1075,6 +1171,7 @@ struct Engine {
         if (!hit) count(L.off_cnt, cid, 0);
         dly += L.access_time;
         int way = set_find(v, L.nways, r.prog);
+        PROF_ADD(LV == 0 ? PF_SETL0 : PF_SETLN, p_set);
         if (way >= 0) {                                      // hit
             set_ts(v, tsa, way, timer + dly);
             hit = true;
@@ -1175,6 +1272,9 @@ struct Engine {
 __device__ __forceinline__ void stats_init() {
     const int ln = lane_id();
     if (ln < SN_COUNT) lds_stat[ln] = 0;
+#ifdef PU_PROF
+    if (ln < PF_COUNT) lds_prof[ln] = 0;
+#endif
     if (ln == 0) lds_err = 0;
     __syncthreads();
 }
@@ -1209,8 +1309,10 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
             if (e.ln == 0) delays[i] = 0;
             continue;
         }
+        PROF_T(p_loop);
         const pu_req q = reqs[i];
         if (q.batch_start) D = 0;
+        PROF_ADD(PF_REQ, p_loop);
         const int64_t t = q.timer + D;
         Req r{q.addr, q.prog_id, (int32_t)q.mem_type};
         int d = e.access(q.core, r, t);
@@ -1225,6 +1327,7 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
             halted = 1;
         }
         if (e.stop) halted = 1;            // engine limit hit (sharer pool): cannot continue exactly
+        PROF_ADD(PF_LOOP, p_loop);
     }
     if (e.ln == 0) {
         rs->batch_delay = D;
@@ -1234,6 +1337,9 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
     }
     __syncthreads();
     e.flush_stats();
+#ifdef PU_PROF
+    if (e.ln < PF_COUNT) atomicAdd(&g_prof[e.ln], lds_prof[e.ln]);
+#endif
 }
 
 // Queue records start as the single free interval [0, UINT64_MAX]
@@ -1295,6 +1401,9 @@ __global__ __launch_bounds__(64) void unit_network_kernel(const Geo* __restrict_
     }
     __syncthreads();
     e.flush_stats();
+#ifdef PU_PROF
+    if (e.ln < PF_COUNT) atomicAdd(&g_prof[e.ln], lds_prof[e.ln]);
+#endif
 }
 
 // Sharer-bitmap pool: free stack [0, P) and RunState.pool_top = P per replica.
@@ -1357,3 +1466,17 @@ extern "C" int pu_engine_init_queues(char* arena, uint64_t replica_bytes, uint64
                        off_qring, nqueues, nreplicas);
     return hipGetLastError() == hipSuccess ? 0 : PU_EIO;
 }
+
+#ifdef PU_PROF
+// Profiling build only: read (and optionally clear) the region counters.
+extern "C" int pu_engine_prof_read(unsigned long long* out, int n, int reset) {
+    if (n > PF_COUNT) n = PF_COUNT;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[PF_COUNT] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return n;
+}
+#endif

@@ -23,7 +23,9 @@ import numpy as np
 from . import _abi as A
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libprimeuncore.so")
+# PRIMEUNCORE_LIB selects another build of the same library (the region-profiling
+# build, tools/prof_regions.py); there is no fallback when it is missing.
+LIB_PATH = os.environ.get("PRIMEUNCORE_LIB") or os.path.join(_HERE, "libprimeuncore.so")
 _lib: Optional[C.CDLL] = None
 
 

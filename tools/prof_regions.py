@@ -1,0 +1,53 @@
+"""Where the engine's time goes: region cycle counters of the profiling build.
+
+Runs bench.py's workload against libprimeuncore_prof.so (make -C
+primesim_amd/csrc prof: the same engine with s_memtime stamps, -DPU_PROF) and
+prints, per region, the summed per-wave cycles and their share of the
+per-request loop.  Regions are inclusive (NET contains NSETUP/NHOPS/NWB, NHOPS
+contains NTREE, NTREE contains NWAIT, HOME contains the transmits it makes).
+
+    python tools/prof_regions.py -- --steps 3 --warmup 1 --no-cpu
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF_LIB = os.path.join(ROOT, "primesim_amd", "libprimeuncore_prof.so")
+NAMES = ["LOOP", "REQ", "NET", "NSETUP", "NHOPS", "NTREE", "NWAIT", "NWB", "SETL0", "SETLN", "HOME_LD",
+         "HOME", "DOWN", "windows", "tree_hops", "demand_hops", "T_LDS", "T_SEARCH", "T_DECIDE", "T_EDIT",
+         "T_STORE", "T_REFILL"]
+COUNTS = {"windows", "tree_hops", "demand_hops"}
+
+
+def main() -> None:
+    if not os.path.exists(PROF_LIB):
+        raise SystemExit(f"{PROF_LIB} missing: make -C primesim_amd/csrc prof")
+    os.environ["PRIMEUNCORE_LIB"] = PROF_LIB
+    sys.path.insert(0, ROOT)
+    args = [a for a in sys.argv[1:] if a != "--"]
+    import bench  # noqa: E402
+    import primesim_amd.uncore as U  # noqa: E402
+
+    sys.argv = ["bench.py", *args]
+    bench.main()
+    L = U.lib()
+    fn = L.pu_engine_prof_read
+    fn.restype = C.c_int
+    fn.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
+    buf = (C.c_ulonglong * len(NAMES))()
+    if fn(buf, len(NAMES), 0) < 0:
+        raise SystemExit("pu_engine_prof_read failed")
+    vals = dict(zip(NAMES, (int(x) for x in buf)))
+    loop = max(vals["LOOP"], 1)
+    out = {}
+    for k, v in vals.items():
+        out[k] = v if k in COUNTS else {"cycles": v, "frac_of_loop": round(v / loop, 4)}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
