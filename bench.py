@@ -8,8 +8,11 @@ DRAM 120 cycles; synthetic stream: 80% uniform over 2^20 lines + 20% over a
 100-request messages, canonical order.
 
 One "step" = every replica on this GPU advances its own request stream by
---chunk requests in one engine launch (the hot path: prime.cpp's message loop
-over System::access).  A replica is one complete, independent 1024-core uncore
+--chunk (40,960) requests in one engine launch (the hot path: prime.cpp's
+message loop over System::access).  A quantum of the C4 stream is ~409,600
+requests (1024 cores x ~400 requests per 1000-cycle quantum), so the default
+10 warmup steps run the first quantum (every core active; cold caches and empty
+link histories) untimed and the 10 timed steps run the second quantum.  A replica is one complete, independent 1024-core uncore
 (its own seed); the engine runs one replica per wavefront and many replicas
 per GPU, because a single uncore is a strictly sequential fold.
 `value` = all requests processed by all ranks / max-over-ranks wall time of the
@@ -17,8 +20,9 @@ K timed steps, with the requests already resident in HBM.
 
 Rank 0 also times the reference's own CPU uncore (oracle/_ref, compiled from
 /root/reference in the build container) — or, if that library is absent, the
-CPU restatement — on a bounded prefix of replica 0's stream on one host core,
-and checks that the GPU's delays for that prefix are bit-identical.
+CPU restatement — on replica 0's stream on one host core: an untimed fill over
+the warmup requests, then timed over the GPU's timed window; it checks that the
+GPU's delays for every request it ran are bit-identical.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 under
 torch.distributed.run (one process per GPU).
@@ -39,6 +43,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 METRIC = "simulated memory accesses/sec (uncore) at 1024 cores; % HBM roofline"
+REQ_BYTES = 32          # sizeof(pu_req)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 
@@ -71,33 +76,37 @@ def sum_stats(um, replicas: int) -> dict:
     return tot
 
 
-def cpu_baseline(cfg_xml: str, cfg, reqs: np.ndarray, threads, budget_s: float):
-    """Time the reference CPU uncore (or the restatement) on a prefix of `reqs`."""
+def cpu_baseline(cfg_xml: str, cfg, reqs: np.ndarray, threads, fill: int, budget_s: float):
+    """Time the reference CPU uncore (or the restatement) on reqs[fill:], after
+    an untimed run over reqs[:fill]; returns every delay it produced."""
     import oracle as O
     kind = "reference" if O.ref_available() else "port"
     eng = O.RefUncore(cfg_xml) if kind == "reference" else O.CpuRef(cfg)
     for prog, th in threads:
         eng.alloc_core(prog, th)
-    chunk = 5000
-    done = 0
+    chunk = 8192
     delays = []
+    for a in range(0, fill, chunk):
+        d, rc = eng.run(reqs[a:min(fill, a + chunk)])
+        delays.append(d)
+    done = fill
     t0 = time.perf_counter()
     while done < len(reqs) and time.perf_counter() - t0 < budget_s:
         d, rc = eng.run(reqs[done:done + chunk])
         delays.append(d)
         done += len(d)
     el = time.perf_counter() - t0
-    return kind, done, el, np.concatenate(delays) if delays else np.zeros(0, np.int32)
+    return kind, done - fill, el, np.concatenate(delays) if delays else np.zeros(0, np.int32)
 
 
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=10, help="timed steps (default: the stream's second quantum)")
+    ap.add_argument("--warmup", type=int, default=10, help="untimed steps (default: the first quantum)")
     ap.add_argument("--replicas", type=int, default=0, help="replicas per GPU (0 = size to HBM)")
-    ap.add_argument("--chunk", type=int, default=2500, help="requests per replica per step")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--chunk", type=int, default=40960, help="requests per replica per step")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) normally; gloo for CPU-side rehearsal")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -127,55 +136,61 @@ def main() -> None:
     CF.write_xml(sim, xml_path)
     cfg = P.load_config(xml_path)
 
-    # ---- size the replica count to HBM (one replica ~= 0.65 GB at C4)
+    # ---- per-replica HBM: engine state + the timed request slabs + one warmup chunk
     um = P.UncoreManager()
     probe = P.UncoreManager()
     probe.init(cfg, replicas=1, device=local)
     rbytes = probe.replica_bytes
     probe.close()
+    per_bytes = rbytes + (args.steps + 1) * args.chunk * (REQ_BYTES + 4)
     free, total = torch.cuda.mem_get_info(dev)
-    R = args.replicas or max(1, min(2048, int((free * 0.85) // rbytes)))
+    R = args.replicas or max(1, min(2048, int((free * 0.88) // per_bytes)))
     R = max(1, R - R % 8) if R >= 8 else R
-    log(f"[bench] rank {rank}: replica {rbytes / 2**20:.0f} MiB, {R} replicas, free {free / 2**30:.0f} GiB")
+    log(f"[bench] rank {rank}: replica {rbytes / 2**20:.0f} MiB + requests {(per_bytes - rbytes) / 2**20:.0f} MiB, "
+        f"{R} replicas, free {free / 2**30:.0f} GiB")
     um.init(cfg, replicas=R, device=local)
-
-    # ---- request streams (one seed per replica, disjoint across ranks), resident in HBM
-    per = args.chunk * (args.warmup + args.steps)
-    streams = []
-    t_gen = time.time()
-    for r in range(R):
-        spec = P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=replica_seed(4, rank, r), num_quanta=64,
-                            max_requests=per)
-        s = P.generate_stream(spec)
-        assert len(s) == per, (len(s), per)
-        streams.append(s)
     threads = P.stream_threads(P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024))
     for prog, th in threads:
         um.allocCore(prog, th)
-    host = np.stack(streams)                       # [R, per] requests
-    log(f"[bench] generated {host.size} requests in {time.time() - t_gen:.1f}s")
-    # step-major layout so each launch reads one contiguous slab: [steps][R][chunk]
-    nsteps = args.warmup + args.steps
-    slab = host.reshape(R, nsteps, args.chunk).transpose(1, 0, 2).copy()
-    d_reqs = torch.from_numpy(slab.view(np.uint8).reshape(-1)).to(dev)
-    d_delay = torch.zeros(nsteps * R * args.chunk, dtype=torch.int32, device=dev)
-    offs = []
-    for s in range(nsteps):
-        o = (np.arange(R + 1, dtype=np.uint64) * args.chunk) + np.uint64(s * R * args.chunk)
-        offs.append(torch.from_numpy(o.astype(np.uint64).view(np.int64)).to(dev))
+
+    # ---- request streams: one seed per replica (disjoint across ranks), produced
+    # chunk by chunk in canonical order by the resumable host generator
+    specs = [P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=replica_seed(4, rank, r), num_quanta=64)
+             for r in range(R)]
+    gen = P.StreamSet(specs)
+    host = np.zeros((R, args.chunk), dtype=A.REQ_DTYPE)
+    offs = torch.from_numpy((np.arange(R + 1, dtype=np.uint64) * np.uint64(args.chunk)).view(np.int64)).to(dev)
     # a dedicated (non-null) stream: the engine launches on it and the HIP
     # events below time exactly those launches
     stream = torch.cuda.Stream(dev)
     sptr = stream.cuda_stream
     assert sptr != 0
+    rep0 = []                                       # replica 0's delays, for the parity check
 
-    def launch(s: int) -> None:
-        um.run_device(d_reqs.data_ptr(), offs[s].data_ptr(), d_delay.data_ptr(), sptr)
+    def next_chunk() -> torch.Tensor:
+        got = gen.next_into(host)
+        assert got == args.chunk, (got, args.chunk)
+        return torch.from_numpy(host.view(np.uint8).reshape(-1)).to(dev)
 
+    # warmup: the first quantum of every replica's stream (all 1024 cores, cold
+    # caches, empty link histories); untimed, requests uploaded step by step
+    d_warm_delay = torch.zeros(R * args.chunk, dtype=torch.int32, device=dev)
+    t_w = time.time()
     for s in range(args.warmup):
-        launch(s)
+        d_req = next_chunk()
+        um.run_device(d_req.data_ptr(), offs.data_ptr(), d_warm_delay.data_ptr(), sptr)
         torch.cuda.synchronize(dev)
-        log(f"[bench] warmup step {s} done")
+        rep0.append(d_warm_delay[:args.chunk].cpu().numpy())
+        del d_req
+        log(f"[bench] warmup step {s} done ({time.time() - t_w:.1f}s)")
+    if os.environ.get("PU_PROF_RESET_AFTER_WARMUP"):   # tools/prof_regions.py: count the timed steps only
+        P.uncore.lib().pu_engine_prof_read(None, 0, 1)
+    # timed: the next `steps` chunks, generated and made resident in HBM first
+    t_gen = time.time()
+    d_reqs = [next_chunk() for _ in range(args.steps)]
+    d_delay = [torch.zeros(R * args.chunk, dtype=torch.int32, device=dev) for _ in range(args.steps)]
+    torch.cuda.synchronize(dev)
+    log(f"[bench] timed requests resident: {args.steps} x {R} x {args.chunk} in {time.time() - t_gen:.1f}s")
     before = sum_stats(um, R)
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -185,7 +200,7 @@ def main() -> None:
     t0 = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record(stream)
-        launch(args.warmup + k)
+        um.run_device(d_reqs[k].data_ptr(), offs.data_ptr(), d_delay[k].data_ptr(), sptr)
         ev[k][1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -193,6 +208,8 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     log(f"[bench] timed {args.steps} steps in {elapsed:.3f}s; per-launch ms {['%.1f' % x for x in kern_ms]}")
+    rep0 += [d[:args.chunk].cpu().numpy() for d in d_delay]
+    gen.close()
 
     after = sum_stats(um, R)
     delta = {k: after[k] - before.get(k, 0) for k in after if k != "error_flags"}
@@ -224,19 +241,20 @@ def main() -> None:
     if rank == 0:
         cpu = None
         if not args.no_cpu:
-            # replica 0's stream, long enough for a time-bounded (~cpu_seconds) sample
-            long0 = P.generate_stream(P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=4, num_quanta=64,
-                                                   max_requests=max(per, 2_000_000)))
-            assert np.array_equal(long0[:per], streams[0])
-            kind, n_cpu, el, d_cpu = cpu_baseline(xml_path, cfg, long0, threads, args.cpu_seconds)
-            # bit-exact check of replica 0's GPU delays on the same prefix
-            gpu_d = d_delay.cpu().numpy().reshape(nsteps, R, args.chunk)[:, 0, :].reshape(-1)
+            # replica 0's stream: the reference fills the warmup quantum untimed,
+            # then is timed on the same requests the GPU's timed region covered
+            w0, n_t = args.warmup * args.chunk, args.steps * args.chunk
+            s0 = P.generate_stream(P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=replica_seed(4, rank, 0),
+                                                num_quanta=64, max_requests=w0 + n_t))
+            kind, n_cpu, el, d_cpu = cpu_baseline(xml_path, cfg, s0, threads, w0, args.cpu_seconds)
+            gpu_d = np.concatenate(rep0)
             m = min(len(d_cpu), len(gpu_d))
             parity = bool(np.array_equal(gpu_d[:m], d_cpu[:m]))
             cpu = {"value": n_cpu / el, "unit": "accesses/s", "cores": 1, "kind": kind,
-                   "sample": f"first {n_cpu} requests of replica 0's C4 stream, single-threaded "
+                   "sample": f"replica 0's C4 stream: requests {w0}..{w0 + n_cpu} (the GPU's timed window, after "
+                             f"an untimed fill of the {w0}-request warmup), single-threaded "
                              f"({'reference uncore compiled from /root/reference/src' if kind == 'reference' else 'oracle/cpu_ref restatement'}), "
-                             f"{el:.1f} s; GPU delays bit-identical on that prefix: {parity} ({m} compared)"}
+                             f"{el:.1f} s; GPU delays bit-identical on all {m} requests compared: {parity}"}
             log(f"[bench] cpu baseline ({kind}): {n_cpu / el:.0f} accesses/s; parity on {m} delays: {parity}")
         result = {
             "metric": METRIC,

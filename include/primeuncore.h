@@ -273,6 +273,20 @@ int64_t pu_stream_generate(const pu_stream_params* p, pu_req* out, size_t cap);
 /* The (prog_id, thread_id) of core c in a generated stream. */
 int pu_stream_thread_of(const pu_stream_params* p, int core, int* prog_id, int* thread_id);
 
+/* Resumable streams: the same requests as pu_stream_generate, produced in
+ * consecutive chunks (concatenating the chunks gives exactly the one-shot
+ * stream).  pu_stream_next returns the number written (< n at the end).
+ * pu_stream_next_many advances `count` streams by up to n_each requests each
+ * on `threads` host threads (<= 0: all cores), stream i writing
+ * out[i*stride ...]; returns the smallest count written. */
+typedef struct pu_stream pu_stream;
+pu_stream* pu_stream_open(const pu_stream_params* p);
+void       pu_stream_close(pu_stream* s);
+int64_t    pu_stream_next(pu_stream* s, pu_req* out, size_t n);
+int64_t    pu_stream_position(const pu_stream* s);
+int64_t    pu_stream_next_many(pu_stream* const* s, int count, pu_req* out, size_t n_each,
+                               size_t stride, int threads);
+
 /* Trace files ("PUTRACE1": header, thread table, pu_req records). */
 int pu_trace_write(const char* path, const pu_req* reqs, size_t n,
                    const int32_t* thread_prog, const int32_t* thread_id, int num_threads);

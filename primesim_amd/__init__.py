@@ -5,8 +5,8 @@ this package is its Python host mirror (`uncore.UncoreManager`), the config_prim
 schema (`config`) and the ctypes ABI definitions (`_abi`).
 """
 from . import _abi, config  # noqa: F401
-from .uncore import (InsMem, StreamSpec, UncoreError, UncoreManager, config_from_dict,  # noqa: F401
+from .uncore import (InsMem, StreamSet, StreamSpec, UncoreError, UncoreManager, config_from_dict,  # noqa: F401
                      generate_stream, load_config, parse_config, stream_threads)
 
-__all__ = ["InsMem", "StreamSpec", "UncoreError", "UncoreManager", "config_from_dict", "generate_stream",
+__all__ = ["InsMem", "StreamSet", "StreamSpec", "UncoreError", "UncoreManager", "config_from_dict", "generate_stream",
            "load_config", "parse_config", "stream_threads"]

@@ -1472,7 +1472,8 @@ extern "C" int pu_engine_init_queues(char* arena, uint64_t replica_bytes, uint64
 extern "C" int pu_engine_prof_read(unsigned long long* out, int n, int reset) {
     if (n > PF_COUNT) n = PF_COUNT;
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+    if (n > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * n) != hipSuccess)
+        return -1;
     if (reset) {
         unsigned long long z[PF_COUNT] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return -1;

@@ -30,6 +30,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/primeuncore.h"
@@ -156,44 +158,73 @@ bool params_ok(const pu_stream_params* p) {
     return true;
 }
 
-// Generates the stream; when out == nullptr only counts.
+// The generator's whole state, so a stream can be produced in consecutive
+// chunks (pu_stream_next) that concatenate to exactly pu_stream_generate's
+// output: per-core RNG/cycle state plus the (quantum, core, message) cursor.
+struct StreamGen {
+    pu_stream_params p{};
+    int wpct = 0;
+    std::vector<CoreGen> gens;
+    int q = 0;            // current quantum
+    int c = 0;            // current core within the quantum
+    int in_msg = 0;       // requests already in the core's open message
+    int64_t n = 0;        // requests produced so far
+    int64_t limit = INT64_MAX;
+
+    void init(const pu_stream_params* pp) {
+        p = *pp;
+        wpct = p.write_pct >= 0 ? p.write_pct : default_write_pct(p.kind);
+        gens.assign((size_t)p.num_cores, CoreGen{});
+        for (int k = 0; k < p.num_cores; k++) gens[(size_t)k].rng.s = p.seed * 0x100000000ull + (uint64_t)k;
+        limit = p.max_requests > 0 ? p.max_requests : INT64_MAX;
+    }
+
+    // Up to `cap` more requests in canonical order (quantum-major, then core
+    // id, message-atomic); out == nullptr only counts.
+    int64_t next(pu_req* out, int64_t cap) {
+        int64_t k = 0;
+        while (q < p.num_quanta && n < limit && k < cap) {
+            const int64_t barrier = (int64_t)(q + 1) * p.quantum;
+            CoreGen& g = gens[(size_t)c];
+            if (g.cycle >= barrier) {          // core c reached the barrier: next core / quantum
+                in_msg = 0;
+                if (++c == p.num_cores) {
+                    c = 0;
+                    q++;
+                }
+                continue;
+            }
+            uint64_t a;
+            uint8_t t;
+            make_request(&p, c, g, wpct, &a, &t);
+            if (out) {
+                pu_req& r = out[k];
+                std::memset(&r, 0, sizeof(r));
+                r.addr = a;
+                r.timer = g.cycle;
+                r.core = c;
+                r.prog_id = prog_of(&p, c);
+                r.mem_type = t;
+                r.batch_start = in_msg == 0 ? 1 : 0;
+            }
+            k++;
+            n++;
+            in_msg = (in_msg + 1) % p.max_msg;
+            g.cycle += 1 + (int64_t)(g.rng.next() & 3);
+        }
+        return k;
+    }
+};
+
+// Generates the whole stream; when out == nullptr only counts.
 int64_t run(const pu_stream_params* p, pu_req* out, size_t cap) {
     if (!params_ok(p)) return PU_EINVAL;
-    int wpct = p->write_pct >= 0 ? p->write_pct : default_write_pct(p->kind);
-    std::vector<CoreGen> gens((size_t)p->num_cores);
-    for (int c = 0; c < p->num_cores; c++) {
-        gens[(size_t)c].rng.s = p->seed * 0x100000000ull + (uint64_t)c;
-    }
-    int64_t n = 0;
-    int64_t limit = p->max_requests > 0 ? p->max_requests : INT64_MAX;
-    for (int q = 0; q < p->num_quanta && n < limit; q++) {
-        int64_t barrier = (int64_t)(q + 1) * p->quantum;
-        for (int c = 0; c < p->num_cores && n < limit; c++) {
-            CoreGen& g = gens[(size_t)c];
-            int in_msg = 0;
-            int prog = prog_of(p, c);
-            while (g.cycle < barrier && n < limit) {
-                uint64_t a;
-                uint8_t t;
-                make_request(p, c, g, wpct, &a, &t);
-                if (out) {
-                    if ((size_t)n >= cap) return PU_ERANGE;
-                    pu_req& r = out[n];
-                    std::memset(&r, 0, sizeof(r));
-                    r.addr = a;
-                    r.timer = g.cycle;
-                    r.core = c;
-                    r.prog_id = prog;
-                    r.mem_type = t;
-                    r.batch_start = in_msg == 0 ? 1 : 0;
-                }
-                n++;
-                in_msg = (in_msg + 1) % p->max_msg;
-                g.cycle += 1 + (int64_t)(g.rng.next() & 3);
-            }
-        }
-    }
-    return n;
+    StreamGen g;
+    g.init(p);
+    if (!out) return g.next(nullptr, INT64_MAX);
+    int64_t got = g.next(out, (int64_t)cap);
+    if (got == (int64_t)cap && g.next(nullptr, 1) != 0) return PU_ERANGE;   // more than cap requests
+    return got;
 }
 
 }  // namespace
@@ -215,6 +246,54 @@ int pu_stream_thread_of(const pu_stream_params* p, int core, int* prog_id, int* 
     if (prog_id) *prog_id = prog;
     if (thread_id) *thread_id = core - first;
     return 0;
+}
+
+struct pu_stream {
+    StreamGen g;
+};
+
+pu_stream* pu_stream_open(const pu_stream_params* p) {
+    if (!params_ok(p)) {
+        pu::set_error(PU_EINVAL, "invalid stream parameters");
+        return nullptr;
+    }
+    pu_stream* s = new (std::nothrow) pu_stream;
+    if (!s) {
+        pu::set_error(PU_ENOMEM, "out of host memory");
+        return nullptr;
+    }
+    s->g.init(p);
+    return s;
+}
+
+void pu_stream_close(pu_stream* s) { delete s; }
+
+int64_t pu_stream_next(pu_stream* s, pu_req* out, size_t n) {
+    if (!s || (!out && n)) return PU_EINVAL;
+    return s->g.next(out, (int64_t)n);
+}
+
+int64_t pu_stream_position(const pu_stream* s) { return s ? s->g.n : PU_EINVAL; }
+
+int64_t pu_stream_next_many(pu_stream* const* s, int count, pu_req* out, size_t n_each, size_t stride,
+                            int threads) {
+    if (!s || count < 0 || (!out && n_each && count) || stride < n_each) return PU_EINVAL;
+    for (int i = 0; i < count; i++)
+        if (!s[i]) return PU_EINVAL;
+    if (threads <= 0) threads = (int)std::thread::hardware_concurrency();
+    if (threads > count) threads = count;
+    if (threads < 1) threads = 1;
+    std::vector<int64_t> got((size_t)count, 0);
+    auto work = [&](int t0) {
+        for (int i = t0; i < count; i += threads) got[(size_t)i] = s[i]->g.next(out + (size_t)i * stride, (int64_t)n_each);
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; t++) pool.emplace_back(work, t);
+    work(0);
+    for (auto& th : pool) th.join();
+    int64_t mn = count ? got[0] : 0;
+    for (int64_t v : got) mn = v < mn ? v : mn;
+    return mn;
 }
 
 int pu_trace_write(const char* path, const pu_req* reqs, size_t n, const int32_t* thread_prog,

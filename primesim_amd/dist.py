@@ -14,8 +14,10 @@ import torch.distributed as dist
 
 
 def replica_seed(base: int, rank: int, replica: int) -> int:
-    """Seed of replica `replica` on `rank`: disjoint across ranks and replicas."""
-    return base + 1000 * rank + replica
+    """Seed of replica `replica` on `rank`: disjoint across ranks and replicas
+    (a rank holds at most 2^16 replicas)."""
+    assert 0 <= replica < (1 << 16)
+    return base + (rank << 16) + replica
 
 
 def reduce_run(elapsed_s: float, processed: int, device: torch.device | None = None) -> tuple[float, int]:

@@ -67,6 +67,11 @@ def lib() -> C.CDLL:
         "pu_stream_count": (C.c_int64, [P(A.StreamParams)]),
         "pu_stream_generate": (C.c_int64, [P(A.StreamParams), C.c_void_p, C.c_size_t]),
         "pu_stream_thread_of": (C.c_int, [P(A.StreamParams), C.c_int, P(C.c_int), P(C.c_int)]),
+        "pu_stream_open": (C.c_void_p, [P(A.StreamParams)]),
+        "pu_stream_close": (None, [C.c_void_p]),
+        "pu_stream_next": (C.c_int64, [C.c_void_p, C.c_void_p, C.c_size_t]),
+        "pu_stream_position": (C.c_int64, [C.c_void_p]),
+        "pu_stream_next_many": (C.c_int64, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.c_size_t, C.c_int]),
         "pu_trace_write": (C.c_int, [C.c_char_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int]),
         "pu_unit_queue_run": (C.c_int, [C.c_uint64, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
                                         P(C.c_uint64), C.c_int]),
@@ -140,6 +145,56 @@ def generate_stream(spec: StreamSpec) -> np.ndarray:
         if got != n:
             raise UncoreError(f"stream generation returned {got}, expected {n}")
     return out
+
+
+class StreamSet:
+    """Resumable generators for several streams (pu_stream_open/next_many):
+    `next(n)` returns the next n requests of every stream as an [count, n]
+    array; the chunks concatenate to exactly generate_stream's output."""
+
+    def __init__(self, specs: list[StreamSpec]):
+        self._h = []
+        for sp in specs:
+            p = sp.params()
+            h = lib().pu_stream_open(C.byref(p))
+            if not h:
+                self.close()
+                raise UncoreError(f"stream: {last_error()}")
+            self._h.append(h)
+        self._arr = (C.c_void_p * len(self._h))(*self._h)
+
+    def __len__(self) -> int:
+        return len(self._h)
+
+    def next_into(self, out: np.ndarray, threads: int = 0) -> int:
+        """Fill out[i, :] with stream i's next out.shape[1] requests; returns the
+        smallest number produced (short only at the end of a stream)."""
+        assert out.dtype == A.REQ_DTYPE and out.ndim == 2 and out.shape[0] == len(self._h)
+        assert out.flags.c_contiguous
+        got = lib().pu_stream_next_many(self._arr, len(self._h), out.ctypes.data, out.shape[1], out.shape[1],
+                                        threads)
+        if got < 0:
+            raise UncoreError(f"stream: {last_error()}")
+        return int(got)
+
+    def next(self, n: int, threads: int = 0) -> np.ndarray:
+        out = np.zeros((len(self._h), n), dtype=A.REQ_DTYPE)
+        got = self.next_into(out, threads)
+        return out[:, :got]
+
+    def position(self, i: int = 0) -> int:
+        return int(lib().pu_stream_position(self._h[i]))
+
+    def close(self) -> None:
+        for h in self._h:
+            lib().pu_stream_close(h)
+        self._h = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def stream_threads(spec: StreamSpec) -> list[tuple[int, int]]:

@@ -58,3 +58,41 @@ def test_thread_map_programs():
     spec = P.StreamSpec(A.PU_STREAM_MULTIPROGRAM, 256, num_progs=4)
     th = P.stream_threads(spec)
     assert th[0] == (1, 0) and th[63] == (1, 63) and th[64] == (2, 0) and th[255] == (4, 63)
+
+
+@pytest.mark.parametrize("chunk", [1, 7, 100, 4096])
+def test_resumable_streams_concatenate_to_one_shot(chunk):
+    """pu_stream_next_many chunks == pu_stream_generate, across quantum and
+    message boundaries, for several streams advanced on several threads."""
+    specs = [P.StreamSpec(k, 48, seed=s, quantum=200, num_quanta=3, max_msg=9, num_progs=2)
+             for s, k in ((1, A.PU_STREAM_UNIFORM_HOTSPOT), (2, A.PU_STREAM_SHARED_UNIFORM),
+                          (3, A.PU_STREAM_MULTIPROGRAM))]
+    want = [P.generate_stream(sp) for sp in specs]
+    ss = P.StreamSet(specs)
+    got = [[] for _ in specs]
+    while True:
+        out = np.zeros((len(specs), chunk), dtype=A.REQ_DTYPE)
+        ss.next_into(out, threads=3)
+        done = True
+        for i in range(len(specs)):
+            n_i = min(chunk, len(want[i]) - sum(len(x) for x in got[i]))
+            if n_i > 0:
+                got[i].append(out[i, :n_i].copy())
+                done = False
+        if done:
+            break
+    for i in range(len(specs)):
+        g = np.concatenate(got[i])
+        np.testing.assert_array_equal(g.view(np.uint8), want[i].view(np.uint8))
+        assert ss.position(i) == len(want[i])
+    assert len(ss.next(5)[0]) == 0          # exhausted
+    ss.close()
+
+
+def test_resumable_stream_respects_max_requests():
+    spec = P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=4, num_quanta=64, max_requests=10_000)
+    ss = P.StreamSet([spec])
+    a = ss.next(6000)[0]
+    b = ss.next(6000)[0]
+    assert len(a) == 6000 and len(b) == 4000
+    np.testing.assert_array_equal(np.concatenate([a, b]).view(np.uint8), P.generate_stream(spec).view(np.uint8))

@@ -27,6 +27,7 @@ def main() -> None:
     if not os.path.exists(PROF_LIB):
         raise SystemExit(f"{PROF_LIB} missing: make -C primesim_amd/csrc prof")
     os.environ["PRIMEUNCORE_LIB"] = PROF_LIB
+    os.environ["PU_PROF_RESET_AFTER_WARMUP"] = "1"
     sys.path.insert(0, ROOT)
     args = [a for a in sys.argv[1:] if a != "--"]
     import bench  # noqa: E402
