@@ -42,6 +42,8 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
+LAST_REPLICAS = 0       # replicas of the last main() run (tools/prof_regions.py)
+LAST_PER_REPLICA = None  # per-replica stat deltas of the timed steps (profiling runs only)
 METRIC = "simulated memory accesses/sec (uncore) at 1024 cores; % HBM roofline"
 REQ_BYTES = 32          # sizeof(pu_req)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
@@ -106,6 +108,9 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=10, help="untimed steps (default: the first quantum)")
     ap.add_argument("--replicas", type=int, default=0, help="replicas per GPU (0 = size to HBM)")
     ap.add_argument("--chunk", type=int, default=40960, help="requests per replica per step")
+    ap.add_argument("--slice-ms", type=float, default=400.0,
+                    help="timed steps are wall-time slices: every replica continues its own stream for this long "
+                         "per launch (stopping only between requests); 0 = fixed --chunk requests per replica per step")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) normally; gloo for CPU-side rehearsal")
@@ -148,6 +153,8 @@ def main() -> None:
     R = max(1, R - R % 8) if R >= 8 else R
     log(f"[bench] rank {rank}: replica {rbytes / 2**20:.0f} MiB + requests {(per_bytes - rbytes) / 2**20:.0f} MiB, "
         f"{R} replicas, free {free / 2**30:.0f} GiB")
+    global LAST_REPLICAS
+    LAST_REPLICAS = R
     um.init(cfg, replicas=R, device=local)
     threads = P.stream_threads(P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024))
     for prog, th in threads:
@@ -185,13 +192,28 @@ def main() -> None:
         log(f"[bench] warmup step {s} done ({time.time() - t_w:.1f}s)")
     if os.environ.get("PU_PROF_RESET_AFTER_WARMUP"):   # tools/prof_regions.py: count the timed steps only
         P.uncore.lib().pu_engine_prof_read(None, 0, 1)
-    # timed: the next `steps` chunks, generated and made resident in HBM first
+    # timed window: the next steps x chunk requests of every replica, generated
+    # and made resident in HBM first, replica-major ([R][steps*chunk])
     t_gen = time.time()
-    d_reqs = [next_chunk() for _ in range(args.steps)]
-    d_delay = [torch.zeros(R * args.chunk, dtype=torch.int32, device=dev) for _ in range(args.steps)]
+    W_t = args.steps * args.chunk
+    d_win = torch.empty((R, W_t, REQ_BYTES), dtype=torch.uint8, device=dev)
+    for k in range(args.steps):
+        d_win[:, k * args.chunk:(k + 1) * args.chunk, :] = next_chunk().view(R, args.chunk, REQ_BYTES)
+    d_win_delay = torch.zeros(R * W_t, dtype=torch.int32, device=dev)
+    win_off = np.arange(R + 1, dtype=np.uint64) * np.uint64(W_t)
+    d_win_off = torch.from_numpy(win_off.view(np.int64)).to(dev)
+    d_pos = torch.from_numpy(win_off[:-1].copy().view(np.int64)).to(dev)
+    # fixed-size steps (--slice-ms 0): launch k covers [k*chunk, (k+1)*chunk) of every replica
+    step_offs = [torch.from_numpy(np.concatenate([[0], win_off[:-1] + np.uint64((k + 1) * args.chunk)])
+                                  .astype(np.uint64).view(np.int64)).to(dev) for k in range(args.steps)]
     torch.cuda.synchronize(dev)
-    log(f"[bench] timed requests resident: {args.steps} x {R} x {args.chunk} in {time.time() - t_gen:.1f}s")
+    log(f"[bench] timed requests resident: {R} x {W_t} in {time.time() - t_gen:.1f}s")
     before = sum_stats(um, R)
+    prof_keys = ("requests", "net_accesses", "net_distance", "mg1_calls", "lockdown_calls", "dram_accesses",
+                 "total_num_broadcast", "L0_miss", "directory_ins", "directory_miss", "net_total_delay")
+    per_before = None
+    if os.environ.get("PU_PROF_RESET_AFTER_WARMUP"):
+        per_before = [um.stats(r).as_dict() for r in range(R)]
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
@@ -199,19 +221,34 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        ev[k][0].record(stream)
-        um.run_device(d_reqs[k].data_ptr(), offs.data_ptr(), d_delay[k].data_ptr(), sptr)
-        ev[k][1].record(stream)
+        if args.slice_ms > 0:
+            ev[k][0].record(stream)
+            um.run_device_sliced(d_win.data_ptr(), d_win_off.data_ptr(), d_win_delay.data_ptr(), d_pos.data_ptr(),
+                                 int(args.slice_ms * 1000), sptr)
+            ev[k][1].record(stream)
+        else:
+            ev[k][0].record(stream)
+            um.run_device_sliced(d_win.data_ptr(), step_offs[k].data_ptr(), d_win_delay.data_ptr(), d_pos.data_ptr(),
+                                 0, sptr)
+            ev[k][1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     log(f"[bench] timed {args.steps} steps in {elapsed:.3f}s; per-launch ms {['%.1f' % x for x in kern_ms]}")
-    rep0 += [d[:args.chunk].cpu().numpy() for d in d_delay]
+    pos = d_pos.cpu().numpy().view(np.uint64)
+    adv = (pos - win_off[:-1]).astype(np.int64)
+    log(f"[bench] requests per replica in the timed window: min {adv.min()} median {int(np.median(adv))} "
+        f"max {adv.max()} of {W_t}")
+    rep0.append(d_win_delay[:int(adv[0])].cpu().numpy())
     gen.close()
 
     after = sum_stats(um, R)
+    if per_before is not None:
+        global LAST_PER_REPLICA
+        per_after = [um.stats(r).as_dict() for r in range(R)]
+        LAST_PER_REPLICA = {k: [int(per_after[r][k] - per_before[r][k]) for r in range(R)] for k in prof_keys}
     delta = {k: after[k] - before.get(k, 0) for k in after if k != "error_flags"}
     errf = after.get("error_flags", 0)
     # requests that actually reached the uncore: a replica whose message delay
@@ -242,7 +279,8 @@ def main() -> None:
         cpu = None
         if not args.no_cpu:
             # replica 0's stream: the reference fills the warmup quantum untimed,
-            # then is timed on the same requests the GPU's timed region covered
+            # then is timed on the requests of the GPU's timed window (as many as
+            # fit in --cpu-seconds); parity is checked on every request both ran
             w0, n_t = args.warmup * args.chunk, args.steps * args.chunk
             s0 = P.generate_stream(P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=replica_seed(4, rank, 0),
                                                 num_quanta=64, max_requests=w0 + n_t))
@@ -251,8 +289,9 @@ def main() -> None:
             m = min(len(d_cpu), len(gpu_d))
             parity = bool(np.array_equal(gpu_d[:m], d_cpu[:m]))
             cpu = {"value": n_cpu / el, "unit": "accesses/s", "cores": 1, "kind": kind,
-                   "sample": f"replica 0's C4 stream: requests {w0}..{w0 + n_cpu} (the GPU's timed window, after "
-                             f"an untimed fill of the {w0}-request warmup), single-threaded "
+                   "sample": f"replica 0's C4 stream: requests {w0}..{w0 + n_cpu} (the GPU's timed window; the GPU "
+                             f"ran {int(adv[0])} of them for replica 0), after an untimed fill of the {w0}-request "
+                             f"warmup, single-threaded "
                              f"({'reference uncore compiled from /root/reference/src' if kind == 'reference' else 'oracle/cpu_ref restatement'}), "
                              f"{el:.1f} s; GPU delays bit-identical on all {m} requests compared: {parity}"}
             log(f"[bench] cpu baseline ({kind}): {n_cpu / el:.0f} accesses/s; parity on {m} delays: {parity}")
@@ -273,7 +312,11 @@ def main() -> None:
                 "workload": "C4: 1024-core 32x32 mesh, L1 32KB/8W + 256KB/8W shared-LLC slice per tile, "
                             "directory MESI full-map, uniform 2^20 lines + 64-line hotspot, 25% writes",
                 "replicas_per_gpu": R,
-                "requests_per_replica_per_step": args.chunk,
+                "step": (f"wall-time slice: every replica continues its own stream for {args.slice_ms:g} ms per "
+                         f"launch, stopping only between requests" if args.slice_ms > 0 else
+                         f"fixed: {args.chunk} requests per replica per launch"),
+                "mean_requests_per_replica_per_step": processed / (R * args.steps),
+                "warmup_requests_per_replica": args.warmup * args.chunk,
                 "parallelism": f"replicas: {R} independent uncores per GPU x {world} GPU(s)",
                 "per_replica_accesses_per_s": value / (R * world),
                 "halted_replicas": halted,

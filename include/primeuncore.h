@@ -218,6 +218,15 @@ int pu_access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n,
  * Nothing is copied to or from the host. */
 int pu_run_device(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off,
                   int32_t* d_delay, void* hip_stream);
+/* Time-sliced variant for throughput runs of many replicas: replica r
+ * processes d_reqs[d_pos[r] .. d_off[r+1]) in order but stops before the first
+ * request that would start more than budget_us microseconds (wall clock) after
+ * its wavefront started, and writes its next position back to d_pos[r]
+ * (device memory, num_replicas entries).  A replica stops only between
+ * requests, so calling again continues its stream exactly; results are the
+ * same as one unsliced run over the same requests.  budget_us = 0: no limit. */
+int pu_run_device_sliced(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off,
+                         int32_t* d_delay, uint64_t* d_pos, uint64_t budget_us, void* hip_stream);
 int pu_synchronize(pu_handle* h);
 
 /* Per-core completion cycle of the last request each core issued

@@ -89,20 +89,13 @@ struct RingView {
     uint64_t lf, ls, hf, hs;
 };
 
-// Uniform copy of a queue header (QueueHdr dwords 0-9).
+// A queue header (QueueHdr dwords 0-13) as held by a lane.
 struct QState {
     uint32_t head, count;
     uint64_t n;
     double sum, sum_sq;
     uint64_t newest;
-};
-
-// A window of up to 64 hops of one route, prefetched with lane h holding hop
-// h: its link id, its header dwords and its two front ring slots.
-struct RouteView {
-    int32_t q;
-    uint32_t d0, d1, d2, d3, d4, d5, d6, d7, d8, d9;
-    uint64_t f0, f1;     // ring[head].first, ring[head+1].first
+    uint64_t f0, f1;
 };
 
 #define AS1 __attribute__((address_space(1)))
@@ -139,6 +132,9 @@ enum ProfId {
 #ifdef PU_PROF
 static __shared__ unsigned long long lds_prof[PF_COUNT];
 __device__ unsigned long long g_prof[PF_COUNT];
+// per-replica (block) wall-clock stamps of the last launch and summed durations
+#define PU_PROF_BLOCKS 4096
+__device__ unsigned long long g_blk_t0[PU_PROF_BLOCKS], g_blk_t1[PU_PROF_BLOCKS], g_blk_dur[PU_PROF_BLOCKS];
 #define PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define PROF_ADD(id, t0) \
     do { if (lane_id() == 0) atomicAdd(&lds_prof[id], (unsigned long long)(__builtin_amdgcn_s_memtime() - (t0))); } while (0)
@@ -223,6 +219,25 @@ __device__ __forceinline__ void ring_shift(uint64_t lo, uint64_t hi, uint64_t& o
     ohi = cross ? (((uint64_t)a1 << 32) | a0) : (((uint64_t)b1 << 32) | b0);
 }
 
+// Inclusive prefix sum of a u64 over the wave (lane 0 first): rows of 16 by
+// row_shr 1/2/4/8, then row_bcast 15/31 across rows.  Lanes a DPP step
+// cannot source from add 0 (the builtin's `old` operand).
+template <int CTRL, int RM>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, RM, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, RM, 0xF, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t scan_incl_u64(uint64_t v) {
+    v += dpp_u64<0x111, 0xF>(v);   // row_shr:1
+    v += dpp_u64<0x112, 0xF>(v);   // row_shr:2
+    v += dpp_u64<0x114, 0xF>(v);   // row_shr:4
+    v += dpp_u64<0x118, 0xF>(v);   // row_shr:8
+    v += dpp_u64<0x142, 0xA>(v);   // row_bcast:15 -> rows 1, 3
+    v += dpp_u64<0x143, 0xC>(v);   // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
 // computeQueueDelay's outcome for interval [f, s] if the search stops there
 // (queue_model_history_tree.cpp:74-106): op 1 second<-t, 2 first<-t+d+p,
 // 3 remove, 4 split; returns the delay d.
@@ -246,7 +261,8 @@ __device__ __forceinline__ uint64_t tree_case(uint64_t f, uint64_t s, uint64_t t
 // written back.  The ring side that moves is the shorter one (a prefix move
 // shifts `head`): only the logical order is observable.
 __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingView& v, uint32_t& head,
-                                            uint32_t& cnt, uint64_t t, uint64_t p, uint64_t minp, uint64_t& err) {
+                                            uint32_t& cnt, uint64_t t, uint64_t p, uint64_t minp, uint64_t& err,
+                                            uint64_t& f0n, uint64_t& f1n) {
     const int ln = lane_id();
     PROF_T(p_s);
     const uint64_t tp = t + p;
@@ -341,6 +357,12 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
     AS1 v2u64* R = q_ring(c, q);
     if (wl) R[ln] = v2u64{lf, ls};
     if (wh) R[ln + 64] = v2u64{hf, hs};
+    // the header's copies of the first two interval starts
+    const uint32_t s0 = head, s1 = (head + 1) & (PU_QRING - 1);
+    const uint64_t a0 = rl64(lf, (int)(s0 & 63)), b0 = rl64(hf, (int)(s0 & 63));
+    const uint64_t a1 = rl64(lf, (int)(s1 & 63)), b1 = rl64(hf, (int)(s1 & 63));
+    f0n = s0 < 64 ? a0 : b0;
+    f1n = s1 < 64 ? a1 : b1;
     PROF_ADD(PF_T_STORE, p_w);
     return d;
 }
@@ -351,7 +373,9 @@ __device__ __forceinline__ void q_store_hdr(const NetCtx& c, int q, const QState
     uint64_t sb = (uint64_t)__double_as_longlong(st.sum), qb = (uint64_t)__double_as_longlong(st.sum_sq);
     *reinterpret_cast<AS1 v4u32*>(H) = v4u32{st.head, st.count, (uint32_t)st.n, (uint32_t)(st.n >> 32)};
     *reinterpret_cast<AS1 v4u32*>(H + 4) = v4u32{(uint32_t)sb, (uint32_t)(sb >> 32), (uint32_t)qb, (uint32_t)(qb >> 32)};
-    *reinterpret_cast<AS1 v2u32*>(H + 8) = v2u32{(uint32_t)st.newest, (uint32_t)(st.newest >> 32)};
+    *reinterpret_cast<AS1 v4u32*>(H + 8) = v4u32{(uint32_t)st.newest, (uint32_t)(st.newest >> 32), (uint32_t)st.f0,
+                                                 (uint32_t)(st.f0 >> 32)};
+    *reinterpret_cast<AS1 v2u32*>(H + 12) = v2u32{(uint32_t)st.f1, (uint32_t)(st.f1 >> 32)};
 }
 
 // M/G/1 update (queue_model_m_g_1.cpp:45-55) and header write-back (lane 0).
@@ -364,52 +388,56 @@ __device__ __forceinline__ void q_finish(const NetCtx& c, int q, QState& st, uin
     if (lane_id() == 0) q_store_hdr(c, q, st);
 }
 
-// One computeQueueDelay given the header and the first two interval starts.
-__device__ __forceinline__ uint64_t q_step(const NetCtx& c, int q, QState& st, uint64_t f0, uint64_t f1, uint64_t t,
-                                           uint64_t p, uint64_t minp, uint64_t& mg1, uint64_t& err) {
-    uint64_t front = f0;
+// One computeQueueDelay on a uniform header (bus queues, unit tests).
+__device__ __forceinline__ uint64_t q_step(const NetCtx& c, int q, QState& st, uint64_t t, uint64_t p, uint64_t minp,
+                                           uint64_t& mg1, uint64_t& err) {
     if (st.count >= PU_QMAX) {      // prune the minimum (history_tree.cpp:49-55)
         st.head = (st.head + 1) & (PU_QRING - 1);
         st.count--;
-        front = f1;
+        st.f0 = st.f1;
     }
     uint64_t d;
-    if (front > t + p) {             // older than the tracked history: M/G/1 (history_tree.cpp:58-63)
+    if (st.f0 > t + p) {             // older than the tracked history: M/G/1 (history_tree.cpp:58-63)
         d = mg1_wait(st);
         mg1++;
     } else {
         RingView v;
         ring_load(c, q, st.head, st.count, v);
-        d = tree_op(c, q, v, st.head, st.count, t, p, minp, err);
+        d = tree_op(c, q, v, st.head, st.count, t, p, minp, err, st.f0, st.f1);
     }
     q_finish(c, q, st, t, p, d);
     return d;
 }
 
-__device__ __forceinline__ QState hdr_state(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t d4,
-                                            uint32_t d5, uint32_t d6, uint32_t d7, uint32_t d8, uint32_t d9) {
+__device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+__device__ __forceinline__ QState hdr_state(v4u32 a, v4u32 b, v4u32 c, v4u32 d) {
     QState st;
-    st.head = d0;
-    st.count = d1;
-    st.n = ((uint64_t)d3 << 32) | d2;
-    st.sum = __longlong_as_double((long long)(((uint64_t)d5 << 32) | d4));
-    st.sum_sq = __longlong_as_double((long long)(((uint64_t)d7 << 32) | d6));
-    st.newest = ((uint64_t)d9 << 32) | d8;
+    st.head = a.x;
+    st.count = a.y;
+    st.n = u64of(a.z, a.w);
+    st.sum = __longlong_as_double((long long)u64of(b.x, b.y));
+    st.sum_sq = __longlong_as_double((long long)u64of(b.z, b.w));
+    st.newest = u64of(c.x, c.y);
+    st.f0 = u64of(c.z, c.w);
+    st.f1 = u64of(d.x, d.y);
     return st;
+}
+__device__ __forceinline__ v4u32 uni4(v4u32 v) { return v4u32{uni32(v.x), uni32(v.y), uni32(v.z), uni32(v.w)}; }
+__device__ __forceinline__ void hdr_load(const NetCtx& c, int q, v4u32& a, v4u32& b, v4u32& cc, v4u32& d) {
+    const AS1 v4u32* H = reinterpret_cast<const AS1 v4u32*>(q_hdr(c, q));
+    a = H[0];
+    b = H[1];
+    cc = H[2];
+    d = H[3];
 }
 
 // A whole queue op loading its own state (bus queues, unit tests).
 __device__ __forceinline__ uint64_t q_op(const NetCtx& c, int q, uint64_t t, uint64_t p, uint64_t minp, uint64_t& mg1,
                                          uint64_t& err) {
-    const AS1 uint32_t* H = q_hdr(c, q);
-    v4u32 a = *reinterpret_cast<const AS1 v4u32*>(H);
-    v4u32 b = *reinterpret_cast<const AS1 v4u32*>(H + 4);
-    v2u32 e = *reinterpret_cast<const AS1 v2u32*>(H + 8);
-    QState st = hdr_state(uni32(a.x), uni32(a.y), uni32(a.z), uni32(a.w), uni32(b.x), uni32(b.y), uni32(b.z),
-                          uni32(b.w), uni32(e.x), uni32(e.y));
-    const AS1 v2u64* R = q_ring(c, q);
-    uint64_t f0 = uni64(R[st.head].x), f1 = uni64(R[(st.head + 1) & (PU_QRING - 1)].x);
-    return q_step(c, q, st, f0, f1, t, p, minp, mg1, err);
+    v4u32 a, b, cc, d;
+    hdr_load(c, q, a, b, cc, d);
+    QState st = hdr_state(uni4(a), uni4(b), uni4(cc), uni4(d));
+    return q_step(c, q, st, t, p, minp, mg1, err);
 }
 
 __device__ __forceinline__ void net_coords(const NetCtx& c, int id, int& x, int& y, int& z) {
@@ -496,16 +524,6 @@ __device__ __forceinline__ void ring_dma(const NetCtx& c, int q, uint32_t head, 
         : "v"(ga), "v"(gb), "s"(lo), "s"(hi)
         : "memory");
 }
-// Stage the ring of window hop jj (its header is in lanes of hhead/hcnt).
-__device__ __forceinline__ void ring_dma_hop(const NetCtx& c, int rq, uint32_t hhead, uint32_t hcnt, int jj,
-                                             int slot) {
-    uint32_t head = rl32(hhead, jj), cnt = rl32(hcnt, jj);
-    if (cnt >= PU_QMAX) {           // the prune this hop will do first
-        head = (head + 1) & (PU_QRING - 1);
-        cnt--;
-    }
-    ring_dma(c, (int)rl32((uint32_t)rq, jj), head, cnt, slot);
-}
 // Wait until at most `n` newer staging rings (2 DMAs each) are still in flight.
 __device__ __forceinline__ void vm_wait_dma(int n) {
     switch (n) {
@@ -560,38 +578,32 @@ __device__ __noinline__ uint64_t net_transmit(char* base_in, uint64_t off_qhdr, 
     for (int b0 = 0; b0 < hops; b0 += 64) {
         PROF_T(p_setup);
         PROF_CNT(PF_WINDOWS, 1);
-        // ---- prefetch the window: lane h = hop b0+h
+        // ---- prefetch the window: lane h = hop b0+h loads its link's header
+        // (one 64-B line: moments, ring cursor, first two interval starts)
         const int h = b0 + ln;
+        const int nh = hops - b0 < 64 ? hops - b0 : 64;
         int rq = 0;
-        v4u32 ha = v4u32{0, 0, 0, 0}, hb = v4u32{0, 0, 0, 0};
-        v2u32 hc = v2u32{0, 0};
-        uint64_t rf0 = 0, rf1 = 0;
+        v4u32 ha = v4u32{0, 0, 0, 0}, hb = ha, hc = ha, hd = ha;
         if (h < hops) {
             rq = net_route_link(c, h, sx, sy, sz, rx, ry, rz, hx, hy);
-            const AS1 uint32_t* H = q_hdr(c, rq);
-            ha = *reinterpret_cast<const AS1 v4u32*>(H);
-            hb = *reinterpret_cast<const AS1 v4u32*>(H + 4);
-            hc = *reinterpret_cast<const AS1 v2u32*>(H + 8);
-            const AS1 v2u64* R = q_ring(c, rq);
-            rf0 = R[ha.x].x;
-            rf1 = R[(ha.x + 1) & (PU_QRING - 1)].x;
+            hdr_load(c, rq, ha, hb, hc, hd);
         }
-        const int nh = hops - b0 < 64 ? hops - b0 : 64;
         // Everything about hop h that does not depend on its arrival time is
         // computed by lane h here, once per window: the prune (history_tree.cpp:
         // 49-55), the front interval, the M/G/1 wait from the pre-update moments
         // (queue_model_m_g_1.cpp:16-42) and the moment updates of q_finish.  The
         // route's links are distinct, so no hop sees another hop's update.
-        uint32_t vhead = ha.x, vcnt = ha.y;
-        uint64_t vfront = rf0;
+        const QState hs = hdr_state(ha, hb, hc, hd);
+        uint32_t vhead = hs.head, vcnt = hs.count;
+        uint64_t vf0 = hs.f0, vf1 = hs.f1;
         if (vcnt >= PU_QMAX) {
             vhead = (vhead + 1) & (PU_QRING - 1);
             vcnt--;
-            vfront = rf1;
+            vf0 = hs.f1;
         }
-        const QState hs = hdr_state(ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w, hc.x, hc.y);
-        const uint64_t vmg1 = ln < nh ? mg1_wait(hs) : 0;
-        uint64_t vfin = 0;              // t + d + p of hop h, filled in by the hop loop
+        const uint64_t vfront = vf0;    // post-prune minimum: the M/G/1 test
+        uint64_t vd = ln < nh ? mg1_wait(hs) : 0;   // hop h's queue delay if it takes M/G/1
+        uint64_t vfin = 0;              // t + d + p of hop h
         // Hop j arrives no earlier than LB_j = t + (j+1)*router + j*link_delay
         // (queue delays are >= 0).  A hop whose front free interval starts by
         // LB_j + p cannot take the M/G/1 branch, so its full ring is certainly
@@ -612,48 +624,64 @@ __device__ __noinline__ uint64_t net_transmit(char* base_in, uint64_t off_qhdr, 
         }
         PROF_ADD(PF_NSETUP, p_setup);
         PROF_T(p_hops);
-        // ---- the arrival-time recurrence, hop by hop
-        for (int j = 0; j < nh; j++) {
-            t += c.router;
-            uint64_t d;
-            if (rl64(vfront, j) > t + (uint64_t)plen) {   // older than the tracked history: M/G/1
-                d = rl64(vmg1, j);
-                mg1++;
-            } else {
-                PROF_T(p_tree);
-                PROF_CNT(PF_TREEHOPS, 1);
-                const int q = (int)rl32((uint32_t)rq, j);
-                uint32_t head = rl32(vhead, j), cnt = rl32(vcnt, j);
-                RingView v;
-                if (mc && j == (int)__builtin_ctzll(mc)) {
-                    // predicted: its ring is (being) staged in LDS slot consumed % PF
-                    mc &= mc - 1;
-                    PROF_T(p_wait);
-                    vm_wait_dma(issued - consumed - 1);
-                    PROF_ADD(PF_NWAIT, p_wait);
-                    ring_from_lds(consumed % PU_RING_PF, v);
-                    consumed++;
-                    d = tree_op(c, q, v, head, cnt, t, (uint64_t)plen, c.link_delay, err);
-                    PROF_T(p_r);
-                    if (mi) {                   // keep PF rings in flight
-                        const int jj = (int)__builtin_ctzll(mi);
-                        mi &= mi - 1;
-                        ring_dma(c, (int)rl32((uint32_t)rq, jj), rl32(vhead, jj), rl32(vcnt, jj),
-                                 issued % PU_RING_PF);
-                        issued++;
-                    }
-                    PROF_ADD(PF_T_REFILL, p_r);
-                } else {                        // not predicted (arrival pushed past the front)
-                    PROF_CNT(PF_DEMAND, 1);
-                    ring_load(c, q, head, cnt, v);
-                    d = tree_op(c, q, v, head, cnt, t, (uint64_t)plen, c.link_delay, err);
-                }
-                vhead = wl32(vhead, head, j);
-                vcnt = wl32(vcnt, cnt, j);
-                PROF_ADD(PF_NTREE, p_tree);
+        // ---- the arrival-time recurrence t_j = t + (j+1)*router + sum_{i<j}(d_i
+        // + link_delay), lane-parallel: assume every remaining hop takes M/G/1
+        // (its delay is then known), get all arrival times with one wave
+        // prefix scan, and find the first hop whose front interval starts by
+        // its arrival + p — the first tree hop.  Hops before it are final;
+        // the tree hop is done by the wave, and the scan restarts after it.
+        int js = 0;
+        while (js < nh) {
+            const bool live = ln >= js && ln < nh;
+            const uint64_t e = live ? vd + c.link_delay + c.router : 0;
+            const uint64_t S = scan_incl_u64(e);
+            const uint64_t A = t + c.router + (S - e);       // arrival of hop ln (after its router)
+            const uint64_t cand = ballot(live && vfront <= A + (uint64_t)plen);
+            const int jt = cand ? (int)__builtin_ctzll(cand) : nh;
+            if (ln >= js && ln < jt) vfin = A + vd + (uint64_t)plen;
+            mg1 += (uint64_t)(jt - js);
+            if (jt == nh) {                                   // the rest of the window is M/G/1
+                t += rl64(S, nh - 1);
+                break;
             }
-            vfin = wl64(vfin, t + d + (uint64_t)plen, j);
-            t += d + c.link_delay;
+            PROF_T(p_tree);
+            PROF_CNT(PF_TREEHOPS, 1);
+            const uint64_t tj = rl64(A, jt);
+            const int q = (int)rl32((uint32_t)rq, jt);
+            uint32_t head = rl32(vhead, jt), cnt = rl32(vcnt, jt);
+            uint64_t f0n, f1n, d;
+            RingView v;
+            if (mc && jt == (int)__builtin_ctzll(mc)) {
+                // predicted: its ring is (being) staged in LDS slot consumed % PF
+                mc &= mc - 1;
+                PROF_T(p_wait);
+                vm_wait_dma(issued - consumed - 1);
+                PROF_ADD(PF_NWAIT, p_wait);
+                ring_from_lds(consumed % PU_RING_PF, v);
+                consumed++;
+                d = tree_op(c, q, v, head, cnt, tj, (uint64_t)plen, c.link_delay, err, f0n, f1n);
+                PROF_T(p_r);
+                if (mi) {                       // keep PF rings in flight
+                    const int jj = (int)__builtin_ctzll(mi);
+                    mi &= mi - 1;
+                    ring_dma(c, (int)rl32((uint32_t)rq, jj), rl32(vhead, jj), rl32(vcnt, jj), issued % PU_RING_PF);
+                    issued++;
+                }
+                PROF_ADD(PF_T_REFILL, p_r);
+            } else {                            // not predicted (arrival pushed past the front)
+                PROF_CNT(PF_DEMAND, 1);
+                ring_load(c, q, head, cnt, v);
+                d = tree_op(c, q, v, head, cnt, tj, (uint64_t)plen, c.link_delay, err, f0n, f1n);
+            }
+            vhead = wl32(vhead, head, jt);
+            vcnt = wl32(vcnt, cnt, jt);
+            vf0 = wl64(vf0, f0n, jt);
+            vf1 = wl64(vf1, f1n, jt);
+            vd = wl64(vd, d, jt);
+            vfin = wl64(vfin, tj + d + (uint64_t)plen, jt);
+            t = tj + d + c.link_delay;
+            js = jt + 1;
+            PROF_ADD(PF_NTREE, p_tree);
         }
         PROF_ADD(PF_NHOPS, p_hops);
         PROF_T(p_wb);
@@ -662,13 +690,19 @@ __device__ __noinline__ uint64_t net_transmit(char* base_in, uint64_t off_qhdr, 
             QState st = hs;
             st.head = vhead;
             st.count = vcnt;
+            st.f0 = vf0;
+            st.f1 = vf1;
             st.sum_sq = st.sum_sq + (double)plen * (double)plen;
             st.sum = st.sum + (double)plen;
             st.n = st.n + 1;
             st.newest = vfin > st.newest ? vfin : st.newest;
             q_store_hdr(c, rq, st);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no staging DMA outlives its window
+        // No drain here: every staged ring was waited for when its hop consumed
+        // it (predicted hops are a subset of the tree hops), and the header
+        // stores' acknowledgements overlap the next window's loads (a wave's
+        // vector memory operations are processed in order, so those loads
+        // see the stores).
         PROF_ADD(PF_NWB, p_wb);
     }
     t += c.router;
@@ -1283,11 +1317,21 @@ __device__ __forceinline__ void stats_init() {
 // processes reqs[off[blockIdx.x] .. off[blockIdx.x+1]) in order: the message
 // loop of prime.cpp:120-137 (D restarts at each batch_start; d = access(core,
 // req, timer + D); D += d - 1).
+//
+// Time-sliced launches (pos != nullptr): replica r starts at pos[r] instead of
+// off[r], stops before the first request that would begin after
+// `budget_ticks` of the s_memrealtime clock (100 MHz) have passed since the
+// wave started, and writes its next position back to pos[r].  A replica only
+// ever stops between requests, so its stream continues exactly in the next
+// launch; the slice keeps every wave busy instead of waiting for the slowest
+// replica of a fixed-size step.
 template <int NL>
 __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, char* __restrict__ arena,
                                                     int replica0, const pu_req* __restrict__ reqs,
                                                     const uint64_t* __restrict__ off,
-                                                    int32_t* __restrict__ delays) {
+                                                    int32_t* __restrict__ delays, uint64_t* __restrict__ pos,
+                                                    uint64_t budget_ticks) {
+    const uint64_t wave_t0 = __builtin_amdgcn_s_memrealtime();
     Engine<NL> e;
     e.g = g;
     e.ln = lane_id();
@@ -1295,6 +1339,9 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
     stats_init();
     e.dly = 0;
     e.hit = false;
+#ifdef PU_PROF
+    const uint64_t blk_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
     RunState* rs = e.template at<RunState>(g->off_run);
     int32_t D = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->batch_delay : 0u, 0);
@@ -1302,9 +1349,11 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
     e.pool_top = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->pool_top : 0u, 0);
     e.stop = false;
     int64_t* completion = e.template at<int64_t>(g->off_completion);
-    const uint64_t b = off[blockIdx.x], end = off[blockIdx.x + 1];
+    const uint64_t b = pos ? pos[blockIdx.x] : off[blockIdx.x], end = off[blockIdx.x + 1];
     uint64_t done = 0;
-    for (uint64_t i = b; i < end; i++) {
+    uint64_t i = b;
+    for (; i < end; i++) {
+        if (budget_ticks && __builtin_amdgcn_s_memrealtime() - wave_t0 >= budget_ticks) break;
         if (halted) {                       // the reference's handler thread has exited
             if (e.ln == 0) delays[i] = 0;
             continue;
@@ -1330,6 +1379,7 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
         PROF_ADD(PF_LOOP, p_loop);
     }
     if (e.ln == 0) {
+        if (pos) pos[blockIdx.x] = i;
         rs->batch_delay = D;
         rs->halted = halted;
         rs->processed += done;
@@ -1339,6 +1389,12 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
     e.flush_stats();
 #ifdef PU_PROF
     if (e.ln < PF_COUNT) atomicAdd(&g_prof[e.ln], lds_prof[e.ln]);
+    if (e.ln == 0 && blockIdx.x < PU_PROF_BLOCKS) {
+        const uint64_t blk_t1 = __builtin_amdgcn_s_memrealtime();
+        g_blk_t0[blockIdx.x] = blk_t0;
+        g_blk_t1[blockIdx.x] = blk_t1;
+        g_blk_dur[blockIdx.x] += blk_t1 - blk_t0;
+    }
 #endif
 }
 
@@ -1358,6 +1414,9 @@ __global__ void init_queues_kernel(char* arena, uint64_t replica_bytes, uint64_t
     h->sum = 0.0;
     h->sum_sq = 0.0;
     h->newest = 0;
+    h->f0 = 0;
+    h->f1 = 0;
+    h->_pad = 0;
     QueueSlot* ring = reinterpret_cast<QueueSlot*>(base + off_qring) + q * PU_QRING;
     ring[0] = QueueSlot{0ull, UINT64_MAX};
 }
@@ -1445,13 +1504,14 @@ extern "C" int pu_engine_unit_network(const Geo* d_geo, char* base, const int32_
 
 // ---------------------------------------------------------------- launchers
 extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,
-                                const pu_req* reqs, const uint64_t* off, int32_t* delays, hipStream_t stream) {
+                                const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
+                                uint64_t budget_ticks, hipStream_t stream) {
     dim3 grid((unsigned)nblocks), block(64);
     switch (num_levels) {
-        case 1: hipLaunchKernelGGL(uncore_kernel<1>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays); break;
-        case 2: hipLaunchKernelGGL(uncore_kernel<2>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays); break;
-        case 3: hipLaunchKernelGGL(uncore_kernel<3>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays); break;
-        case 4: hipLaunchKernelGGL(uncore_kernel<4>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays); break;
+        case 1: hipLaunchKernelGGL(uncore_kernel<1>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays, pos, budget_ticks); break;
+        case 2: hipLaunchKernelGGL(uncore_kernel<2>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays, pos, budget_ticks); break;
+        case 3: hipLaunchKernelGGL(uncore_kernel<3>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays, pos, budget_ticks); break;
+        case 4: hipLaunchKernelGGL(uncore_kernel<4>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays, pos, budget_ticks); break;
         default: return PU_EINVAL;
     }
     return hipGetLastError() == hipSuccess ? 0 : PU_EIO;
@@ -1477,7 +1537,19 @@ extern "C" int pu_engine_prof_read(unsigned long long* out, int n, int reset) {
     if (reset) {
         unsigned long long z[PF_COUNT] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return -1;
+        static unsigned long long zb[PU_PROF_BLOCKS];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_blk_dur), zb, sizeof(zb)) != hipSuccess) return -1;
     }
+    return n;
+}
+// Per-block stamps (s_memrealtime, 100 MHz) of the last launch and summed durations.
+extern "C" int pu_engine_prof_blocks(unsigned long long* t0, unsigned long long* t1, unsigned long long* dur, int n) {
+    if (n > PU_PROF_BLOCKS) n = PU_PROF_BLOCKS;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    size_t b = sizeof(unsigned long long) * (size_t)n;
+    if (hipMemcpyFromSymbol(t0, HIP_SYMBOL(g_blk_t0), b) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(t1, HIP_SYMBOL(g_blk_t1), b) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(dur, HIP_SYMBOL(g_blk_dur), b) != hipSuccess) return -1;
     return n;
 }
 #endif

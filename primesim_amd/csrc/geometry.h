@@ -17,7 +17,9 @@
 //     pool     : pool_entries x nwords x u64 bitmaps + a free stack
 //     dalive, dcnt : per slice
 //   queues (Graphite history tree restated as a ring of sorted free intervals):
-//     qhdr : nqueues x QueueHdr (64 B)   — links first, then per-cache buses
+//     qhdr : nqueues x QueueHdr (64 B, one line: M/G/1 moments, ring cursor and
+//            the first two interval starts, so the M/G/1-vs-tree decision of a
+//            hop needs this line only)  — links first, then per-cache buses
 //     qring: nqueues x 128 x {first,second} (2 KB)
 //   stats (EngineStats), per-core completion cycles, run state.
 //
@@ -61,7 +63,11 @@ struct QueueHdr {
     double sum;        // _sigma_service_time
     double sum_sq;     // _sigma_service_time_square
     uint64_t newest;   // _newest_arrival_time
-    uint64_t _pad[3];
+    uint64_t f0;       // ring[head].first: the tree's minimum key (the M/G/1 test)
+    uint64_t f1;       // ring[head+1].first: the minimum after a prune; valid
+                       // whenever count >= PU_QMAX (only a tree op raises count,
+                       // and it refreshes f0/f1 from the ring it holds)
+    uint64_t _pad;
 };
 
 struct QueueSlot {

@@ -27,7 +27,8 @@
 #include "geometry.h"
 
 extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,
-                                const pu_req* reqs, const uint64_t* off, int32_t* delays, hipStream_t stream);
+                                const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
+                                uint64_t budget_ticks, hipStream_t stream);
 extern "C" int pu_engine_init_pool(char* arena, uint64_t replica_bytes, uint64_t off_pool_free, uint64_t off_run,
                                    int pool_entries, int nreplicas, hipStream_t stream);
 extern "C" int pu_engine_unit_queue(const Geo* d_geo, char* base, uint64_t minp, const uint64_t* t,
@@ -241,9 +242,10 @@ int ensure_stage(pu_handle* h, size_t n) {
 }
 
 int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
-           hipStream_t s) {
+           hipStream_t s, uint64_t* d_pos = nullptr, uint64_t budget_ticks = 0) {
     HIP_TRY(hipEventRecord(h->ev0, s), PU_EIO);
-    int rc = pu_engine_launch(h->d_geo, h->geo.num_levels, h->arena, replica0, nblocks, d_reqs, d_off, d_delay, s);
+    int rc = pu_engine_launch(h->d_geo, h->geo.num_levels, h->arena, replica0, nblocks, d_reqs, d_off, d_delay, d_pos,
+                              budget_ticks, s);
     if (rc) return pu::set_error(rc, "engine launch failed");
     HIP_TRY(hipEventRecord(h->ev1, s), PU_EIO);
     return 0;
@@ -425,6 +427,14 @@ int pu_run_device(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
     std::lock_guard<std::mutex> lk(h->mu);
     return launch(h, 0, h->R, d_reqs, d_off, d_delay, s);
+}
+
+int pu_run_device_sliced(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
+                         uint64_t* d_pos, uint64_t budget_us, void* hip_stream) {
+    if (!h || !d_reqs || !d_off || !d_delay || !d_pos) return pu::set_error(PU_EINVAL, "bad arguments");
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    std::lock_guard<std::mutex> lk(h->mu);
+    return launch(h, 0, h->R, d_reqs, d_off, d_delay, s, d_pos, budget_us * 100);   // s_memrealtime: 100 MHz
 }
 
 int pu_synchronize(pu_handle* h) {

@@ -57,6 +57,8 @@ def lib() -> C.CDLL:
         "pu_access": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, P(C.c_uint64), C.c_int64]),
         "pu_access_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.c_void_p]),
         "pu_run_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+        "pu_run_device_sliced": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                           C.c_void_p]),
         "pu_synchronize": (C.c_int, [C.c_void_p]),
         "pu_core_completion": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
         "pu_stats_get": (C.c_int, [C.c_void_p, C.c_int, P(A.Stats)]),
@@ -293,6 +295,15 @@ class UncoreManager:
         rc = lib().pu_run_device(self._handle(), d_reqs_ptr, d_off_ptr, d_delay_ptr, stream_ptr or None)
         if rc != 0:
             raise UncoreError(f"run_device: {last_error()}")
+
+    def run_device_sliced(self, d_reqs_ptr: int, d_off_ptr: int, d_delay_ptr: int, d_pos_ptr: int, budget_us: int,
+                          stream_ptr: int = 0) -> None:
+        """Time-sliced run: replica r continues from d_pos[r] for at most budget_us
+        of wall time (stopping only between requests) and advances d_pos[r]."""
+        rc = lib().pu_run_device_sliced(self._handle(), d_reqs_ptr, d_off_ptr, d_delay_ptr, d_pos_ptr, budget_us,
+                                        stream_ptr or None)
+        if rc != 0:
+            raise UncoreError(f"run_device_sliced: {last_error()}")
 
     def synchronize(self) -> None:
         if lib().pu_synchronize(self._handle()) != 0:

@@ -147,3 +147,49 @@ def test_thread_sched_mirror():
         assert um.deallocCore(7, 0) == 0          # core_stat == 7 != 1: not freed (thread_sched.cpp:81)
     finally:
         um.close()
+
+
+def test_time_sliced_runs_continue_streams_exactly():
+    """pu_run_device_sliced: replicas stop between requests when their slice
+    runs out and continue from d_pos in the next launch; the concatenated
+    delays, counters and completion cycles equal the CPU restatement's."""
+    cfg = P.config_from_dict(CF.preset("C2"))
+    R, n = 10, 4000
+    specs = [P.StreamSpec(A.PU_STREAM_SHARED_UNIFORM, 64, seed=300 + r, max_requests=n) for r in range(R)]
+    streams = [P.generate_stream(s) for s in specs]
+    dev = torch.device("cuda", 0)
+    um = P.UncoreManager()
+    um.init(cfg, replicas=R)
+    try:
+        for prog, th in P.stream_threads(specs[0]):
+            um.allocCore(prog, th)
+        host = np.concatenate(streams)
+        off = (np.arange(R + 1, dtype=np.uint64) * np.uint64(n))
+        d_reqs = torch.from_numpy(host.view(np.uint8).copy()).to(dev)
+        d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+        d_pos = torch.from_numpy(off[:-1].copy().view(np.int64)).to(dev)
+        d_del = torch.full((R * n,), -7, dtype=torch.int32, device=dev)
+        s = torch.cuda.Stream(dev)
+        launches = 0
+        while True:
+            um.run_device_sliced(d_reqs.data_ptr(), d_off.data_ptr(), d_del.data_ptr(), d_pos.data_ptr(), 300,
+                                 s.cuda_stream)
+            torch.cuda.synchronize(dev)
+            launches += 1
+            pos = d_pos.cpu().numpy().view(np.uint64)
+            assert np.all(pos >= off[:-1]) and np.all(pos <= off[1:])
+            if np.array_equal(pos, off[1:]):
+                break
+            assert launches < 10000
+        assert launches > 2, "a 300-us slice should not cover 4000 requests"
+        got = d_del.cpu().numpy().reshape(R, n)
+        for r in (0, 3, R - 1):
+            want, ref = _oracle_run(cfg, specs[r], streams[r])
+            np.testing.assert_array_equal(got[r], want, err_msg=f"replica {r}")
+            gs, ws = um.stats(r).as_dict(), ref.stats().as_dict()
+            assert {k: gs[k] for k in ws if k != "requests"} == {k: ws[k] for k in ws if k != "requests"}
+            np.testing.assert_array_equal(um.completion(r), ref.completion())
+        for r in range(R):
+            assert um.stats(r).requests == n
+    finally:
+        um.close()

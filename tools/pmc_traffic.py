@@ -83,7 +83,7 @@ def main():
     f_kb = sum(fetch[i] for i in timed) / steps
     w_kb = sum(write[i] for i in timed) / steps
     R = bench_line["config"]["replicas_per_gpu"]
-    chunk = bench_line["config"]["requests_per_replica_per_step"]
+    chunk = bench_line["config"]["mean_requests_per_replica_per_step"]
     accesses = R * chunk
     raw = (f_kb + w_kb) * 1024.0
     upper = (2.0 * f_kb + w_kb) * 1024.0

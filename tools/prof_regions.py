@@ -47,6 +47,32 @@ def main() -> None:
     out = {}
     for k, v in vals.items():
         out[k] = v if k in COUNTS else {"cycles": v, "frac_of_loop": round(v / loop, 4)}
+    # per-replica balance: summed per-block durations of the timed launches and
+    # the last launch's start/end spread (s_memrealtime ticks, 100 MHz)
+    R = min(4096, bench.LAST_REPLICAS or 0)
+    if R:
+        import numpy as np
+        t0 = (C.c_ulonglong * R)()
+        t1 = (C.c_ulonglong * R)()
+        du = (C.c_ulonglong * R)()
+        fb = L.pu_engine_prof_blocks
+        fb.restype = C.c_int
+        fb.argtypes = [C.POINTER(C.c_ulonglong)] * 3 + [C.c_int]
+        if fb(t0, t1, du, R) == R:
+            a0, a1, d = (np.array(list(x), dtype=np.float64) for x in (t0, t1, du))
+            span = a1.max() - a0.min()
+            if bench.LAST_PER_REPLICA is not None:
+                dump = {k: np.array(v) for k, v in bench.LAST_PER_REPLICA.items()}
+                dump["timed_dur_ticks"] = d
+                np.savez(os.path.join(ROOT, "gpurun_out", "per_replica.npz"), **dump)
+            out["blocks"] = {
+                "replicas": R,
+                "last_launch_span_ms": span / 1e5,
+                "last_launch_end_ms_pcts": {p: float(np.percentile(a1 - a0.min(), p) / 1e5) for p in (0, 10, 50, 90, 99, 100)},
+                "last_launch_start_ms_max": float((a0.max() - a0.min()) / 1e5),
+                "timed_dur_ms_pcts": {p: float(np.percentile(d, p) / 1e5) for p in (0, 10, 50, 90, 99, 100)},
+                "busy_fraction_last_launch": float((a1 - a0).sum() / (span * R)),
+            }
     print(json.dumps(out, indent=1))
 
 
