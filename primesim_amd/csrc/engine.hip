@@ -543,11 +543,13 @@ __device__ __forceinline__ void ring_from_lds(int slot, RingView& v) {
     v = RingView{a.x, a.y, b.x, b.y};
 }
 
-// Network::transmit (network.cpp:97-160).  Out of line (one copy), every
-// argument made wave-uniform so the hop loop runs on SGPRs and scalar branches.
+// Network::transmit (network.cpp:97-160).  Inlined (a call would wait for every
+// outstanding store at entry and reload a spilled register at exit); every
+// argument is made wave-uniform so the hop loop runs on SGPRs and scalar
+// branches.  The protocol code reaches it from four sites only.
 // Lane h prefetches hop h's link header and the two interval starts at its
 // ring head; only hops taking the tree branch fetch their full ring.
-__device__ __noinline__ uint64_t net_transmit(char* base_in, uint64_t off_qhdr, uint64_t off_qring, uint64_t router,
+__device__ __forceinline__ uint64_t net_transmit(char* base_in, uint64_t off_qhdr, uint64_t off_qring, uint64_t router,
                                               uint64_t link_delay, uint64_t inject, int header_flits, int data_width,
                                               int w, int net_type, int src, int dst, int len, uint64_t timer) {
     NetCtx c;
@@ -978,59 +980,66 @@ struct Engine {
         sh = idx;
     }
 
-    // home -> sharer -> inval -> home for every sharer in ascending id
-    // (system.cpp:605-618, 660-671, 766-779, 820-831)
-    __device__ int inval_sharers(uint32_t nsh, uint64_t sh, int home, const Req& r, int64_t base_t) {
+    // ------------------------------------------------------------ probes from home
+    // Every message exchange a home slice starts with other caches has the
+    // same shape: for each target p in order, home -> p, share/inval down p's
+    // hierarchy, p -> home (reply_len bytes), t_p = pipe + those delays, the
+    // result the max over targets, pipe += header_flits per target
+    // (system.cpp:605-633, 660-671, 687-705, 766-795, 820-831, 846-866).  The
+    // single owner (first_sharer) of an M/E line is a one-target probe.  One
+    // loop serves all of them, so the two transmits below are the only ones
+    // the home code inlines.
+    enum ProbeMode { PR_NONE, PR_ONE, PR_INLINE, PR_POOL, PR_ALL };
+    // Returns the home's delay after the probe.  The owner case accumulates
+    // into `delay` directly (delay += ...; timer + delay), a sharer set adds
+    // the max over targets (initialised to 0) of times relative to
+    // timer + delay: the two differ once an int wraps, so both are kept.
+    __device__ int probe(int mode, int one, uint32_t nsh, uint64_t sh, bool inval, int reply_len, int home,
+                         const Req& r, int64_t timer, int delay) {
         constexpr int last = NL - 1;
-        int pipe = 0, mx = 0;
-        if (nsh == PU_SH_POOL) {
-            uint64_t rem = pool_word(sh);
-            while (true) {
-                uint64_t m = ballot(rem != 0);
+        const bool single = mode == PR_ONE;
+        const int64_t base_t = single ? timer : timer + delay;
+        int pipe = single ? delay : 0, mx = 0;
+        uint64_t rem = mode == PR_POOL ? pool_word(sh) : 0ull;   // lane k: bitmap word k
+        uint32_t k = 0;
+        while (true) {
+            int p;
+            if (mode == PR_ONE) {
+                if (k) break;
+                p = one;
+            } else if (mode == PR_INLINE) {
+                if (k >= nsh) break;
+                p = (int)((sh >> (16 * k)) & 0xFFFF);
+            } else if (mode == PR_POOL) {
+                const uint64_t m = ballot(rem != 0);
                 if (!m) break;
-                int k = (int)__builtin_ctzll(m);
-                int p = k * 64 + (int)__builtin_ctzll(rl64(rem, k));
-                if (ln == k) rem &= rem - 1;
-                int t = pipe;
-                t += (int)transmit(home, p, 0, (uint64_t)(base_t + t));
-                t += down<last, true>(p, r);
-                t += (int)transmit(p, home, 0, (uint64_t)(base_t + t));
-                mx = t > mx ? t : mx;
-                pipe += g->header_flits;
+                const int w = (int)__builtin_ctzll(m);
+                p = w * 64 + (int)__builtin_ctzll(rl64(rem, w));
+                if (ln == w) rem &= rem - 1;
+            } else if (mode == PR_ALL) {
+                if ((int)k >= g->num_cores) break;
+                p = (int)k;
+            } else {
+                break;
             }
-        } else {
-            for (uint32_t i = 0; i < nsh; i++) {
-                int p = (int)((sh >> (16 * i)) & 0xFFFF);
-                int t = pipe;
-                t += (int)transmit(home, p, 0, (uint64_t)(base_t + t));
-                t += down<last, true>(p, r);
-                t += (int)transmit(p, home, 0, (uint64_t)(base_t + t));
-                mx = t > mx ? t : mx;
-                pipe += g->header_flits;
-            }
-        }
-        return mx;
-    }
-    // broadcast to every core (system.cpp:621-633 etc.; N == num_cores enforced)
-    __device__ int broadcast(int home, const Req& r, int64_t base_t) {
-        constexpr int last = NL - 1;
-        int pipe = 0, mx = 0;
-        stat_add(SN_BCAST, 1);
-        for (int i = 0; i < g->num_cores; i++) {
+            k++;
             int t = pipe;
-            t += (int)transmit(home, i, 0, (uint64_t)(base_t + t));
-            t += down<last, true>(i, r);
-            t += (int)transmit(i, home, 0, (uint64_t)(base_t + t));
+            t += (int)transmit(home, p, 0, (uint64_t)(base_t + t));
+            t += inval ? down<last, true>(p, r) : down<last, false>(p, r);
+            t += (int)transmit(p, home, reply_len, (uint64_t)(base_t + t));
+            if (single) return t;
             mx = t > mx ? t : mx;
             pipe += g->header_flits;
         }
-        return mx;
+        return delay + mx;
     }
 
     // ------------------------------------------------------------ home slice
     // accessSharedCache (system.cpp:734-893) / accessDirectoryCache (577-731).
     // The home line is read once (lane w: way w, 32 B) and written once at the
-    // end: nothing reached from here touches directory lines.
+    // end: nothing reached from here touches directory lines.  Every branch
+    // that messages other caches does so first, at timer + access_time, so
+    // the branch only chooses the probe; `probe` runs it.
     __device__ int access_home(int cid, int home, const Req& r, int64_t timer, uint32_t* out_state) {
         PROF_T(p0);
         int d = access_home_impl(cid, home, r, timer, out_state);
@@ -1062,6 +1071,14 @@ struct Engine {
         int delay = D.access_time;
         uint32_t st, nsh;
         uint64_t sh;
+        // the probe this transition makes, and what follows it
+        int pmode = PR_NONE, pone = 0, preply = 0;
+        bool pinval = true;
+        uint32_t psh_n = 0;
+        uint64_t psh = 0;
+        Req pr = r;
+        int extra_dram = 0;      // dram() after the probe: 1 = counted only, 2 = counted and timed
+        bool release_set = false, miss_fill = false;
         if (way < 0 && r.type != PU_WB) {
             // replaceLine (cache.cpp:204-235): first invalid way, else LRU
             const uint64_t inv = ballot(mine && m.state == ST_I);
@@ -1090,26 +1107,22 @@ struct Engine {
             sh = rl64(m.sh, way);
             if (old_st != ST_I) {
                 count(D.off_cnt, home, 2);
-                Req o{old_addr, old_prog, PU_RD};
+                pr = Req{old_addr, old_prog, PU_RD};
                 if (old_st == ST_M || old_st == ST_E) {
-                    int own = first_sharer(nsh, sh);
-                    delay += (int)transmit(home, own, 0, (uint64_t)(timer + delay));
-                    delay += down<last, true>(own, o);
-                    int reply = (!shared || old_st == ST_M) ? blk : 0;
-                    delay += (int)transmit(own, home, reply, (uint64_t)(timer + delay));
-                    dram();
+                    pmode = PR_ONE;
+                    pone = first_sharer(nsh, sh);
+                    preply = (!shared || old_st == ST_M) ? blk : 0;
+                    extra_dram = 1;
                 } else if (old_st == ST_S) {
-                    delay += inval_sharers(nsh, sh, home, o, timer + delay);
+                    pmode = nsh == PU_SH_POOL ? PR_POOL : PR_INLINE;
                 } else if (old_st == ST_B) {
-                    delay += broadcast(home, o, timer + delay);
+                    pmode = PR_ALL;
                 }
             }
             st = r.type == PU_WR ? ST_M : ST_E;
             count(D.off_cnt, home, 1);
-            pool_release(nsh, sh);            // sharer_set.clear(); insert(cache_id)
-            nsh = 1;
-            sh = (uint64_t)cid;
-            delay += dram();
+            release_set = true;
+            miss_fill = true;
         } else if (way < 0) {
             err_or(PU_ERRF_WB_MISS);         // WB missed at home: NULL deref in the reference (Q13)
             *out_state = ST_I;
@@ -1120,27 +1133,24 @@ struct Engine {
             sh = rl64(m.sh, way);
             if (r.type == PU_WR) {
                 if (st == ST_M || st == ST_E) {
-                    int own = first_sharer(nsh, sh);
-                    delay += (int)transmit(home, own, 0, (uint64_t)(timer + delay));
-                    delay += down<last, true>(own, r);
-                    delay += (int)transmit(own, home, blk, (uint64_t)(timer + delay));
+                    pmode = PR_ONE;
+                    pone = first_sharer(nsh, sh);
+                    preply = blk;
                 } else if (st == ST_S) {
-                    delay += inval_sharers(nsh, sh, home, r, timer + delay);
-                    if (!shared) delay += dram();
+                    pmode = nsh == PU_SH_POOL ? PR_POOL : PR_INLINE;
+                    if (!shared) extra_dram = 2;
                 } else if (st == ST_B) {
-                    delay += broadcast(home, r, timer + delay);
-                    if (!shared) delay += dram();
+                    pmode = PR_ALL;
+                    if (!shared) extra_dram = 2;
                 }
                 st = ST_M;
-                pool_release(nsh, sh);
-                nsh = 1;
-                sh = (uint64_t)cid;
+                release_set = true;
             } else if (r.type == PU_RD) {
                 if (st == ST_M || st == ST_E) {
-                    int own = first_sharer(nsh, sh);
-                    delay += (int)transmit(home, own, 0, (uint64_t)(timer + delay));
-                    delay += down<last, false>(own, r);
-                    delay += (int)transmit(own, home, blk, (uint64_t)(timer + delay));
+                    pmode = PR_ONE;
+                    pone = first_sharer(nsh, sh);
+                    preply = blk;
+                    pinval = false;                  // share, not inval (system.cpp:660-671)
                     st = ST_S;
                 } else if (st == ST_S) {
                     if (!shared) delay += dram();
@@ -1150,7 +1160,6 @@ struct Engine {
                 } else if (st == ST_V) {
                     st = ST_E;
                 }
-                add_sharer(nsh, sh, cid);
             } else {
                 st = shared ? ST_V : ST_I;
                 pool_release(nsh, sh);
@@ -1158,6 +1167,23 @@ struct Engine {
                 sh = 0;
                 dram();
             }
+        }
+        if (pmode != PR_NONE) {
+            if (pmode == PR_ALL) stat_add(SN_BCAST, 1);
+            psh_n = nsh;
+            psh = sh;
+            delay = probe(pmode, pone, psh_n, psh, pinval, preply, home, pr, timer, delay);
+        }
+        if (extra_dram == 1) dram();
+        if (extra_dram == 2) delay += dram();
+        if (release_set) {                   // sharer_set.clear(); insert(cache_id)
+            pool_release(nsh, sh);
+            nsh = 1;
+            sh = (uint64_t)cid;
+            if (miss_fill) delay += dram();
+
+        } else if (r.type == PU_RD) {
+            add_sharer(nsh, sh, cid);
         }
         *out_state = st == ST_B ? ST_S : st;
         if (ln == way) {
@@ -1183,6 +1209,9 @@ struct Engine {
 
     // ------------------------------------------------------------ directory MESI walk
     // System::mesi_directory (system.cpp:372-482); LV is the level of `cid`.
+    // Each level calls its parent from one place, and the last level runs its
+    // home transactions (write-back, request/reply, or the S->M upgrade) from
+    // one loop, so the transmit and home-slice code is inlined once.
     template <int LV>
     __device__ uint32_t mesi(int cid, const Req& r, int64_t timer) {
         const LevelGeo& L = g->lv[LV];
@@ -1206,67 +1235,92 @@ struct Engine {
         dly += L.access_time;
         int way = set_find(v, L.nways, r.prog);
         PROF_ADD(LV == 0 ? PF_SETL0 : PF_SETLN, p_set);
+        bool is_miss = false, call_parent = false;
+        int64_t ptimer = 0;
+        uint32_t ret = ST_M;
+        // home transactions of the last level: [0] write-back of the victim
+        // (delays discarded, Q3), [1] the request (or the S->M upgrade)
+        bool tx_wb = false, tx_req = false;
+        int wb_home = 0, req_reply = 0;
+        Req wb_req = r;
         if (way >= 0) {                                      // hit
             set_ts(v, tsa, way, timer + dly);
             hit = true;
-            uint32_t st = rl32(v.mst, way);
+            const uint32_t st = rl32(v.mst, way);
             if (r.type == PU_WR) {
                 if constexpr (!kLast) {
                     if (st != ST_M) {
                         set_state(v, meta, way, ST_I);
-                        int parent = cid * L.share / g->lv[LV + 1].share;
-                        uint32_t ns = mesi<LV + 1>(parent, r, timer + dly);
-                        set_state(v, meta, way, ns);
+                        call_parent = true;
+                        ptimer = timer + dly;
                     }
                 } else {
                     if (st == ST_S) {
-                        int home = home_of(r.addr);
-                        uint32_t tmp;
-                        dly += (int)transmit(cid, home, 0, (uint64_t)(timer + dly));
-                        dly += access_home(cid, home, r, timer + dly, &tmp);
-                        dly += (int)transmit(home, cid, 0, (uint64_t)(timer + dly));
+                        tx_req = true;
+                        req_reply = 0;
                     }
-                    set_state(v, meta, way, ST_M);
                 }
-                return ST_M;
+                ret = ST_M;
+            } else {
+                if (st != ST_S) dly += children<LV, false>(cid, r);
+                return ST_S;
             }
-            if (st != ST_S) dly += children<LV, false>(cid, r);
-            return ST_S;
-        }
-        // miss
-        uint32_t old_st;
-        uint64_t old_addr;
-        int old_prog;
-        way = set_replace(v, meta, L.nways, L.offbits, L.idxbits, r.prog, &old_st, &old_addr, &old_prog);
-        if (old_st != ST_I) {
-            count(L.off_cnt, cid, 2);
-            Req o{old_addr, old_prog, PU_RD};
-            dly += children<LV, true>(cid, o);
-            if (old_st == ST_M || old_st == ST_E) {
-                count(L.off_cnt, cid, 3);
-                if constexpr (kLast) {                       // write-back; delays discarded (Q3)
-                    int home = home_of(old_addr);
-                    o.type = PU_WB;
-                    uint32_t tmp;
-                    transmit(cid, home, (int)L.block, (uint64_t)(timer + dly));
-                    access_home(cid, home, o, timer + dly, &tmp);
+        } else {                                             // miss
+            is_miss = true;
+            uint32_t old_st;
+            uint64_t old_addr;
+            int old_prog;
+            way = set_replace(v, meta, L.nways, L.offbits, L.idxbits, r.prog, &old_st, &old_addr, &old_prog);
+            if (old_st != ST_I) {
+                count(L.off_cnt, cid, 2);
+                Req o{old_addr, old_prog, PU_RD};
+                dly += children<LV, true>(cid, o);
+                if (old_st == ST_M || old_st == ST_E) {
+                    count(L.off_cnt, cid, 3);
+                    if constexpr (kLast) {
+                        tx_wb = true;
+                        wb_home = home_of(old_addr);
+                        wb_req = Req{old_addr, old_prog, PU_WB};
+                    }
                 }
             }
+            set_ts(v, tsa, way, timer + dly);
+            if constexpr (!kLast) {
+                call_parent = true;
+                ptimer = timer;                               // `timer`, not timer+delay (Q2)
+            } else {
+                tx_req = true;
+                req_reply = (int)L.block;
+            }
         }
-        set_ts(v, tsa, way, timer + dly);
-        uint32_t res;
         if constexpr (!kLast) {
-            int parent = cid * L.share / g->lv[LV + 1].share;
-            res = mesi<LV + 1>(parent, r, timer);            // `timer`, not timer+delay (Q2)
+            if (call_parent) {
+                const int parent = cid * L.share / g->lv[LV + 1].share;
+                const uint32_t ns = mesi<LV + 1>(parent, r, ptimer);
+                set_state(v, meta, way, ns);
+                if (is_miss) ret = ns;
+            }
         } else {
-            int home = home_of(r.addr);
-            dly += (int)transmit(cid, home, 0, (uint64_t)(timer + dly));
-            dly += access_home(cid, home, r, timer + dly, &res);
-            dly += (int)transmit(home, cid, (int)L.block, (uint64_t)(timer + dly));
+            const int req_home = home_of(r.addr);
+            for (int k = tx_wb ? 0 : 1; k < (tx_req ? 2 : 1); k++) {
+                const bool wb = k == 0;
+                const int home = wb ? wb_home : req_home;
+                const Req& q = wb ? wb_req : r;
+                const int to_len = wb ? (int)L.block : 0;
+                const int d1 = (int)transmit(cid, home, to_len, (uint64_t)(timer + dly));
+                if (!wb) dly += d1;
+                uint32_t hs;
+                const int d2 = access_home(cid, home, q, timer + dly, &hs);
+                if (!wb) {
+                    dly += d2;
+                    dly += (int)transmit(home, cid, req_reply, (uint64_t)(timer + dly));
+                    if (is_miss) ret = hs;
+                }
+            }
+            set_state(v, meta, way, is_miss ? ret : ST_M);
         }
-        set_state(v, meta, way, res);
-        count(L.off_cnt, cid, 1);
-        return res;
+        if (is_miss) count(L.off_cnt, cid, 1);
+        return ret;
     }
 
     // System::access (system.cpp:144-168), directory system, TLB off.
