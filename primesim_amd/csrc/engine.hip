@@ -152,6 +152,8 @@ struct NetCtx {
     uint64_t off_qhdr, off_qring;
     uint64_t router, link_delay, inject;
     int header_flits, data_width, w, net_type;
+    uint64_t w_magic, w2_magic;
+    int w2, blk_len, plen_blk;
 };
 
 __device__ __forceinline__ AS1 v2u64* q_ring(const NetCtx& c, int q) {
@@ -440,15 +442,22 @@ __device__ __forceinline__ uint64_t q_op(const NetCtx& c, int q, uint64_t t, uin
     return q_step(c, q, st, t, p, minp, mg1, err);
 }
 
+// n / d for n < 2^16 as a multiply-high by m = ceil(2^32 / d) (exact there:
+// n * (m*d - 2^32) < 2^32); uniform operands stay on the scalar unit.
+__device__ __forceinline__ uint32_t div_magic(uint32_t n, uint64_t m) { return (uint32_t)(((uint64_t)n * m) >> 32); }
 __device__ __forceinline__ void net_coords(const NetCtx& c, int id, int& x, int& y, int& z) {
-    const int w = c.w;
+    const uint32_t w = (uint32_t)c.w;
     if (c.net_type == 1) {
-        x = (id % (w * w)) % w;
-        y = (id % (w * w)) / w;
-        z = id / (w * w);
+        const uint32_t zq = div_magic((uint32_t)id, c.w2_magic);
+        const uint32_t rem = (uint32_t)id - zq * (uint32_t)c.w2;
+        const uint32_t yq = div_magic(rem, c.w_magic);
+        x = (int)(rem - yq * w);
+        y = (int)yq;
+        z = (int)zq;
     } else {
-        x = id % w;
-        y = id / w;
+        const uint32_t yq = div_magic((uint32_t)id, c.w_magic);
+        x = (int)((uint32_t)id - yq * w);
+        y = (int)yq;
         z = 0;
     }
 }
@@ -549,27 +558,34 @@ __device__ __forceinline__ void ring_from_lds(int slot, RingView& v) {
 // branches.  The protocol code reaches it from four sites only.
 // Lane h prefetches hop h's link header and the two interval starts at its
 // ring head; only hops taking the tree branch fetch their full ring.
-__device__ __forceinline__ uint64_t net_transmit(char* base_in, uint64_t off_qhdr, uint64_t off_qring, uint64_t router,
-                                              uint64_t link_delay, uint64_t inject, int header_flits, int data_width,
-                                              int w, int net_type, int src, int dst, int len, uint64_t timer) {
+__device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char* base_in, int src, int dst, int len,
+                                                 uint64_t timer) {
     NetCtx c;
     c.base = (AS1 char*)(char*)uni64((uint64_t)base_in);
-    c.off_qhdr = uni64(off_qhdr);
-    c.off_qring = uni64(off_qring);
-    c.router = uni64(router);
-    c.link_delay = uni64(link_delay);
-    c.inject = uni64(inject);
-    c.header_flits = (int)uni32((uint32_t)header_flits);
-    c.data_width = (int)uni32((uint32_t)data_width);
-    c.w = (int)uni32((uint32_t)w);
-    c.net_type = (int)uni32((uint32_t)net_type);
+    c.off_qhdr = g->off_qhdr;
+    c.off_qring = g->off_qring;
+    c.router = g->router_delay;
+    c.link_delay = g->link_delay;
+    c.inject = g->inject_delay;
+    c.header_flits = g->header_flits;
+    c.data_width = g->data_width;
+    c.w = g->net_width;
+    c.net_type = g->net_type;
+    c.w_magic = g->w_magic;
+    c.w2_magic = g->w2_magic;
+    c.w2 = g->w2;
+    c.blk_len = g->blk_len;
+    c.plen_blk = g->plen_blk;
     src = (int)uni32((uint32_t)src);
     dst = (int)uni32((uint32_t)dst);
     len = (int)uni32((uint32_t)len);
     timer = uni64(timer);
     if (src == dst) return 0;
     const int ln = lane_id();
-    const int plen = c.header_flits + (int)ceil((double)len / (double)c.data_width);
+    // network.cpp:104 packet length; the engine only sends 0-byte and block messages
+    const int plen = len == 0 ? c.header_flits
+                   : len == c.blk_len ? c.plen_blk
+                   : c.header_flits + (int)ceil((double)len / (double)c.data_width);
     int sx, sy, sz, rx, ry, rz;
     net_coords(c, src, sx, sy, sz);
     net_coords(c, dst, rx, ry, rz);
@@ -757,8 +773,7 @@ struct Engine {
     }
     __device__ __forceinline__ uint64_t transmit(int src, int dst, int len, uint64_t timer) {
         PROF_T(p0);
-        uint64_t d = net_transmit(base, g->off_qhdr, g->off_qring, g->router_delay, g->link_delay, g->inject_delay,
-                                  g->header_flits, g->data_width, g->net_width, g->net_type, src, dst, len, timer);
+        uint64_t d = net_transmit(g, base, src, dst, len, timer);
         PROF_ADD(PF_NET, p0);
         return d;
     }

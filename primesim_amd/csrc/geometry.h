@@ -37,6 +37,18 @@
 #define PU_MAX_WAYS 64
 #define PU_MAX_NWORDS 64      // sharer bitmap words -> up to 4096 LLC nodes
 
+// Network geometry helpers shared by host and engine.
+static inline void pu_set_net_magic(int w, int header_flits, int data_width, int blk_len, uint64_t* w_magic,
+                                    uint64_t* w2_magic, int32_t* w2, int32_t* blk, int32_t* plen_blk) {
+    const uint64_t ww = (uint64_t)w * (uint64_t)w;
+    *w_magic = ((1ull << 32) + (uint64_t)w - 1) / (uint64_t)w;
+    *w2_magic = ((1ull << 32) + ww - 1) / ww;
+    *w2 = (int32_t)ww;
+    *blk = blk_len;
+    // network.cpp:104: header_flits + (int)ceil((double)data_len / data_width), integer form
+    *plen_blk = blk_len >= 0 ? header_flits + (blk_len + data_width - 1) / data_width : 0;
+}
+
 struct LineMeta {
     uint64_t tag;
     int32_t id;
@@ -103,7 +115,10 @@ struct Geo {
     int32_t max_num_sharers, shared_llc, tlb_enable, dram_access_time;
     int32_t bus_latency, N, net_type, net_width;
     int32_t header_flits, data_width, nlinks, nqueues;
-    int32_t home_offbits, home_mask_bits, _pad0, _pad1;
+    int32_t home_offbits, home_mask_bits;
+    int32_t blk_len, plen_blk;      // last-level block size and its packet length (header + ceil(blk/dw))
+    uint64_t w_magic, w2_magic;     // ceil(2^32 / w), ceil(2^32 / w^2): node id -> mesh coordinates
+    int32_t w2, _pad0;              // (exact division by multiply-high for ids < 2^16)
     uint64_t router_delay, link_delay, inject_delay;
     LevelGeo lv[4];
     DirGeo dir;

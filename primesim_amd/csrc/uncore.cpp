@@ -145,6 +145,8 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
     g->link_delay = y.network.link_delay;
     g->inject_delay = y.network.inject_delay;
     const int w = g->net_width;
+    pu_set_net_magic(w, g->header_flits, g->data_width, (int)g->lv[y.num_levels - 1].block, &g->w_magic,
+                     &g->w2_magic, &g->w2, &g->blk_len, &g->plen_blk);
     g->nlinks = w > 1 ? (w - 1) * w * (g->net_type == 1 ? 3 * w : 2) : 0;
     g->nqueues = g->nlinks + nbus;
     for (int l = 0; l < y.num_levels; l++)
@@ -713,6 +715,7 @@ int pu_unit_network_run(int num_nodes, int net_type, int data_width, int header_
     g.link_delay = link_delay;
     g.inject_delay = inject_delay;
     const int w = g.net_width;
+    pu_set_net_magic(w, header_flits, data_width, -1, &g.w_magic, &g.w2_magic, &g.w2, &g.blk_len, &g.plen_blk);
     g.nlinks = w > 1 ? (w - 1) * w * (net_type == 1 ? 3 * w : 2) : 0;
     g.nqueues = g.nlinks;
     Layout lay;
