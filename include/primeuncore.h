@@ -173,6 +173,8 @@ typedef struct pu_stats {
 #define PU_ERRF_NEG_DELAY    (1ull << 4)  /* batch delay went negative (prime.cpp:130) */
 #define PU_ERRF_POOL         (1ull << 5)  /* sharer-bitmap pool exhausted (engine limit;
                                              raise PRIMEUNCORE_POOL_ENTRIES) */
+#define PU_ERRF_PAGES        (1ull << 6)  /* page table 3/4 full (engine limit;
+                                             raise PRIMEUNCORE_PAGE_ENTRIES) */
 
 /* ------------------------------------------------------------------------
  * Engine lifetime and the hot path.

@@ -25,6 +25,7 @@ PU_ERRF_EMPTY_SHARER = 1 << 2
 PU_ERRF_QUEUE = 1 << 3
 PU_ERRF_NEG_DELAY = 1 << 4
 PU_ERRF_POOL = 1 << 5
+PU_ERRF_PAGES = 1 << 6
 
 
 class CacheCfg(C.Structure):

@@ -749,6 +749,8 @@ struct Engine {
     bool hit;
     int32_t pool_top;    // sharer-bitmap pool stack (RunState.pool_top)
     bool stop;           // replica must stop (pool exhausted)
+    uint64_t page_next;  // RunState.page_next
+    uint64_t last_addr;  // RunState.last_addr
 
 
     template <class T>
@@ -1338,8 +1340,214 @@ struct Engine {
         return ret;
     }
 
-    // System::access (system.cpp:144-168), directory system, TLB off.
-    __device__ int access(int core, const Req& r, int64_t timer) {
+    // ------------------------------------------------------------ snoopy bus MESI walk
+    // System::mesi_bus (system.cpp:224-368); LV is the level of `cid`.  The
+    // share/inval of children is done for its state changes only: mesi_bus
+    // never adds those delays.  Evict/write-back counters are not kept on this
+    // path (Q17).
+    //
+    // Snoop of the other last-level caches for r's line, ascending cache id
+    // (system.cpp:264-276, 311-329, 335-354).  Lane k probes cache base+k's set
+    // (first matching way, like Cache::accessLine), 64 caches per round trip;
+    // holders are then handled in order.  mode 0: write hit in S — every holder
+    // -> I, inval below; 1: write miss — holder inval below, -> I, stop at the
+    // first M/E holder; 2: read miss — share below, -> S, stop at the first
+    // M/E holder.  Returns whether any cache held the line.  (The reference
+    // also creates every cache it snoops; a never-created cache holds no line
+    // and mesi_bus discards the delays where that would show, so the engine
+    // does not mark them.)
+    __device__ bool snoop(int cid, const Req& r, int mode) {
+        constexpr int last = NL - 1;
+        const LevelGeo& L = g->lv[last];
+        LineMeta* meta = at<LineMeta>(L.off_meta);
+        const uint64_t set = (r.addr >> L.offbits) % L.nsets;
+        const uint64_t tag = r.addr >> (L.offbits + L.idxbits);
+        bool any = false;
+        for (int base = 0; base < L.ncaches; base += 64) {
+            const int c = base + ln;
+            int myway = -1;
+            uint32_t myst = ST_I;
+            if (c < L.ncaches && c != cid) {
+                const LineMeta* sp = meta + ((uint64_t)c * L.nsets + set) * L.nways;
+                for (uint64_t w = L.nways; w-- > 0;) {      // lowest matching way wins
+                    const LineMeta m = sp[w];
+                    if (m.state != ST_I && m.id == r.prog && m.tag == tag) {
+                        myway = (int)w;
+                        myst = m.state;
+                    }
+                }
+            }
+            uint64_t hits = ballot(myway >= 0);
+            while (hits) {
+                const int k = (int)__builtin_ctzll(hits);
+                hits &= hits - 1;
+                const int i = base + k;
+                const int way = (int)rl32((uint32_t)myway, k);
+                const uint32_t st = rl32(myst, k);
+                any = true;
+                if (mode == 2) children<last, false>(i, r);
+                else children<last, true>(i, r);
+                if (ln == 0) meta[((uint64_t)i * L.nsets + set) * L.nways + (uint64_t)way].state = mode == 2 ? ST_S : ST_I;
+                if (mode != 0 && (st == ST_M || st == ST_E)) return any;
+            }
+        }
+        return any;
+    }
+
+    template <int LV>
+    __device__ uint32_t mesi_bus(int cid, const Req& r, int64_t timer) {
+        const LevelGeo& L = g->lv[LV];
+        constexpr bool kLast = LV == NL - 1;
+        LineMeta* meta = at<LineMeta>(L.off_meta);
+        int64_t* tsa = at<int64_t>(L.off_ts);
+        SetView v;
+        set_load(v, meta, tsa, L.nsets, L.nways, L.offbits, L.idxbits, (uint64_t)cid, r.addr);
+        mark_alive(LV, cid);
+        if (L.has_bus) {              // Bus::access (bus.cpp:55-61)
+            stat_add(SN_BUSACC, 1);
+            uint64_t bl = (uint64_t)g->bus_latency, mg1 = 0, err = 0;
+            int db = (int)q_op(net_ctx(), L.bus_q0 + cid, (uint64_t)(timer + dly), bl, bl, mg1, err);
+            stat_add(SN_MG1, mg1);
+            if (err) err_or(err);
+            stat_add(SN_BUSCONT, (uint64_t)(int64_t)db);
+            dly += db;
+        }
+        dly += L.access_time;
+        if (!hit) count(L.off_cnt, cid, 0);
+        int way = set_find(v, L.nways, r.prog);
+        bool is_miss = false, call_parent = false;
+        int snoop_mode = -1;
+        uint32_t ret = ST_M;
+        if (way >= 0) {                                      // hit
+            set_ts(v, tsa, way, timer + dly);
+            hit = true;
+            const uint32_t st = rl32(v.mst, way);
+            if (r.type != PU_WR) {
+                if (st != ST_S) children<LV, false>(cid, r);   // share_children, delay discarded
+                return ST_S;
+            }
+            if constexpr (!kLast) {
+                if (st != ST_M) {
+                    set_state(v, meta, way, ST_I);
+                    call_parent = true;
+                }
+            } else {
+                if (st == ST_S) snoop_mode = 0;
+            }
+        } else {                                             // miss
+            is_miss = true;
+            uint32_t old_st;
+            uint64_t old_addr;
+            int old_prog;
+            way = set_replace(v, meta, L.nways, L.offbits, L.idxbits, r.prog, &old_st, &old_addr, &old_prog);
+            if (old_st != ST_I) {
+                Req o{old_addr, old_prog, PU_RD};
+                children<LV, true>(cid, o);                  // inval_children, delay discarded
+            }
+            set_ts(v, tsa, way, timer + dly);
+            if constexpr (!kLast) call_parent = true;
+            else snoop_mode = r.type == PU_WR ? 1 : 2;
+        }
+        if constexpr (!kLast) {
+            if (call_parent) {
+                const int parent = cid * L.share / g->lv[LV + 1].share;
+                const uint32_t ns = mesi_bus<LV + 1>(parent, r, timer + dly);   // timer + delay here
+                set_state(v, meta, way, ns);
+                if (is_miss) ret = ns;
+            }
+        } else {
+            bool shared_line = false;
+            if (snoop_mode >= 0) shared_line = snoop(cid, r, snoop_mode);
+            if (is_miss) {
+                ret = r.type == PU_WR ? ST_M : (shared_line ? ST_S : ST_E);
+                set_state(v, meta, way, ret);
+                dly += dram();
+            } else {
+                set_state(v, meta, way, ST_M);
+            }
+        }
+        if (is_miss) {
+            count(L.off_cnt, cid, 1);
+            return ret;
+        }
+        children<LV, true>(cid, r);                          // write hit: inval_children, discarded
+        return ST_M;
+    }
+
+    // ------------------------------------------------------------ TLB + page table
+    // PageTable::translate (page_table.cpp:56-72): physical pages are numbered
+    // by first touch of (prog, vpage) in processing order.  Open addressing,
+    // linear probing, no deletion: lane k reads slot h+k, so one round trip
+    // covers 64 probe positions; the key is present iff it appears before the
+    // first empty slot.
+    __device__ uint64_t page_translate(int prog, uint64_t vpage) {
+        const TlbGeo& T = g->tlb;
+        PageEnt* tab = at<PageEnt>(T.off_pages);
+        const uint64_t mask = T.pages_cap - 1;
+        uint64_t x = vpage * 0x9E3779B97F4A7C15ull ^ ((uint64_t)(uint32_t)prog * 0xC2B2AE3D27D4EB4Full);
+        x ^= x >> 31;
+        x *= 0xBF58476D1CE4E5B9ull;
+        x ^= x >> 29;
+        uint64_t h = x & mask;
+        for (uint64_t done = 0; done < T.pages_cap; done += 64) {
+            const uint64_t slot = (h + (uint64_t)ln) & mask;
+            const PageEnt e = tab[slot];
+            const bool used = e.used != 0;
+            const uint64_t mm = ballot(used && e.vpage == vpage && e.prog == prog);
+            const uint64_t me = ballot(!used);
+            const int fe = me ? (int)__builtin_ctzll(me) : 64;
+            if (mm && (int)__builtin_ctzll(mm) < fe) return rl64(e.ppage, (int)__builtin_ctzll(mm));
+            if (me) {
+                if (page_next * 4 >= T.pages_cap * 3) {       // keep probes short; engine limit
+                    err_or(PU_ERRF_PAGES);
+                    stop = true;
+                }
+                const uint64_t pp = page_next++;
+                if (ln == fe) tab[slot] = PageEnt{vpage, prog, 1u, pp, 0ull};
+                return pp;
+            }
+            h = (h + 64) & mask;
+        }
+        err_or(PU_ERRF_PAGES);
+        stop = true;
+        return 0;
+    }
+
+    // System::tlb_translate (system.cpp:897-918): private TLB per core; the
+    // request's address becomes physical (ppage << log2(page) | offset).
+    __device__ int tlb_translate(int core, Req& r, int64_t timer) {
+        const TlbGeo& T = g->tlb;
+        LineMeta* meta = at<LineMeta>(T.off_meta);
+        int64_t* tsa = at<int64_t>(T.off_ts);
+        uint64_t* ppa = at<uint64_t>(T.off_ppage);
+        SetView v;
+        set_load(v, meta, tsa, T.nsets, T.nways, T.offbits, T.idxbits, (uint64_t)core, r.addr);
+        const uint64_t mypp = (uint64_t)ln < T.nways ? ppa[v.line0 + (uint64_t)ln] : 0ull;
+        count(T.off_cnt, core, 0);
+        int d = T.access_time;
+        int way = set_find(v, T.nways, r.prog);
+        uint64_t ppage;
+        if (way < 0) {
+            uint32_t old_st;
+            uint64_t old_addr;
+            int old_prog;
+            way = set_replace(v, meta, T.nways, T.offbits, T.idxbits, r.prog, &old_st, &old_addr, &old_prog);
+            if (old_st != ST_I) count(T.off_cnt, core, 2);
+            count(T.off_cnt, core, 1);
+            set_state(v, meta, way, ST_V);
+            ppage = page_translate(r.prog, r.addr >> T.offbits);
+            if (ln == way) ppa[v.line0 + (uint64_t)way] = ppage;
+            d += T.page_miss_delay;
+        } else {
+            ppage = rl64(mypp, way);
+        }
+        set_ts(v, tsa, way, timer);
+        r.addr = (ppage << T.offbits) | (r.addr % T.page_size);
+        return d;
+    }
+
+    // System::access (system.cpp:144-168).
+    __device__ int access(int core, const Req& r_in, int64_t timer) {
         if (core < 0 || core >= g->num_cores) {
             err_or(PU_ERRF_CORE_RANGE);
             return -1;
@@ -1347,7 +1555,13 @@ struct Engine {
         stat_add(SN_REQS, 1);
         hit = false;
         dly = 0;
-        mesi<0>(core, r, timer + dly);
+        Req r = r_in;
+        if (g->tlb_enable) {
+            dly = tlb_translate(core, r, timer);
+            last_addr = r.addr;
+        }
+        if (g->sys_type == 0) mesi<0>(core, r, timer + dly);
+        else mesi_bus<0>(core, r, timer + dly);
         return dly;
     }
 
@@ -1416,6 +1630,8 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
     int32_t D = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->batch_delay : 0u, 0);
     int32_t halted = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->halted : 0u, 0);
     e.pool_top = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->pool_top : 0u, 0);
+    e.page_next = rl64(e.ln == 0 ? rs->page_next : 0ull, 0);
+    e.last_addr = rl64(e.ln == 0 ? rs->last_addr : 0ull, 0);
     e.stop = false;
     int64_t* completion = e.template at<int64_t>(g->off_completion);
     const uint64_t b = pos ? pos[blockIdx.x] : off[blockIdx.x], end = off[blockIdx.x + 1];
@@ -1453,6 +1669,8 @@ __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, c
         rs->halted = halted;
         rs->processed += done;
         rs->pool_top = e.pool_top;
+        rs->page_next = e.page_next;
+        rs->last_addr = e.last_addr;
     }
     __syncthreads();
     e.flush_stats();
@@ -1501,6 +1719,8 @@ __global__ __launch_bounds__(64) void unit_queue_kernel(const Geo* __restrict__ 
     e.base = base;
     e.pool_top = 0;
     e.stop = false;
+    e.page_next = 0;
+    e.last_addr = 0;
     const NetCtx c = e.net_ctx();
     uint64_t calls = 0, err = 0;
     for (uint64_t i = 0; i < n; i++) {
@@ -1523,6 +1743,8 @@ __global__ __launch_bounds__(64) void unit_network_kernel(const Geo* __restrict_
     stats_init();
     e.pool_top = 0;
     e.stop = false;
+    e.page_next = 0;
+    e.last_addr = 0;
     for (uint64_t i = 0; i < n; i++) {
         uint64_t d = e.transmit(src[i], dst[i], len[i], timer[i]);
         if (e.ln == 0) out[i] = d;

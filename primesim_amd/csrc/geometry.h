@@ -110,6 +110,24 @@ struct DirGeo {
     uint64_t off_line, off_pool, off_pool_free, off_alive, off_cnt;
 };
 
+// Per-core TLBs and the first-touch page table (reference system.cpp:897-918,
+// page_table.cpp:56-72): TLB sets like a data cache (LineMeta + ts) plus the
+// physical page per way; the page map is an open-addressing table of
+// PageEnt (linear probing, never deleted), numbered in processing order.
+struct TlbGeo {
+    uint64_t nsets, nways, page_size;
+    int32_t offbits, idxbits, access_time, page_miss_delay;
+    uint64_t off_meta, off_ts, off_ppage, off_cnt;
+    uint64_t off_pages, pages_cap;    // pages_cap: power of two
+};
+struct PageEnt {
+    uint64_t vpage;
+    int32_t prog;
+    uint32_t used;
+    uint64_t ppage;
+    uint64_t _pad;
+};
+
 struct Geo {
     int32_t num_cores, num_levels, sys_type, protocol_type;
     int32_t max_num_sharers, shared_llc, tlb_enable, dram_access_time;
@@ -122,6 +140,7 @@ struct Geo {
     uint64_t router_delay, link_delay, inject_delay;
     LevelGeo lv[4];
     DirGeo dir;
+    TlbGeo tlb;
     uint64_t off_qhdr, off_qring, off_stats, off_completion, off_run;
     uint64_t replica_bytes;
 };
@@ -135,4 +154,6 @@ struct RunState {
     uint64_t processed;    // requests processed so far
     int32_t pool_top;      // free entries on the sharer-bitmap pool stack
     int32_t _pad;
+    uint64_t page_next;    // PageTable::empty_page_num (pages allocated so far)
+    uint64_t last_addr;    // address of the last request after translation (InsMem::addr_dmem)
 };

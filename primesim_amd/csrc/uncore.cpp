@@ -11,6 +11,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -74,10 +75,8 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
     const pu_sys_cfg& y = c->sys;
     if (y.num_levels < 1 || y.num_levels > PU_MAX_LEVELS) return pu::set_error(PU_EINVAL, "num_levels must be 1..4");
     if (y.num_cores < 1) return pu::set_error(PU_EINVAL, "num_cores must be >= 1");
-    if (y.sys_type != 0)
-        return pu::set_error(PU_ENOTSUP, "sys_type=1 (mesi_bus, system.cpp:224) is not implemented by the HIP engine yet");
-    if (y.tlb_enable)
-        return pu::set_error(PU_ENOTSUP, "tlb_enable=1 (system.cpp:897) is not implemented by the HIP engine yet");
+    if (y.sys_type != 0 && y.sys_type != 1) return pu::set_error(PU_EINVAL, "sys_type must be 0 (directory) or 1 (bus)");
+    const bool bus_sys = y.sys_type == 1;
     g->num_cores = y.num_cores;
     g->num_levels = y.num_levels;
     g->sys_type = y.sys_type;
@@ -133,7 +132,7 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
     if (D.nwords > PU_MAX_NWORDS) return pu::set_error(PU_ENOTSUP, "at most 4096 LLC nodes");
     if (y.protocol_type == 1 && N != y.num_cores)
         return pu::set_error(PU_EINVAL, "limited-pointer broadcast needs one LLC per core (system.cpp:623)");
-    if (y.network.link_delay < 1) return pu::set_error(PU_EINVAL, "link_delay must be >= 1");
+    if (!bus_sys && y.network.link_delay < 1) return pu::set_error(PU_EINVAL, "link_delay must be >= 1");
     if (y.network.data_width < 1) return pu::set_error(PU_EINVAL, "data_width must be >= 1");
     g->home_offbits = ilog2(dc.block_size);
     g->home_mask_bits = (int)std::ceil(std::log2((double)N));
@@ -147,8 +146,29 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
     const int w = g->net_width;
     pu_set_net_magic(w, g->header_flits, g->data_width, (int)g->lv[y.num_levels - 1].block, &g->w_magic,
                      &g->w2_magic, &g->w2, &g->blk_len, &g->plen_blk);
-    g->nlinks = w > 1 ? (w - 1) * w * (g->net_type == 1 ? 3 * w : 2) : 0;
+    // the bus system never transmits (mesi_bus has no network), so it keeps no link queues
+    g->nlinks = bus_sys ? 0 : (w > 1 ? (w - 1) * w * (g->net_type == 1 ? 3 * w : 2) : 0);
     g->nqueues = g->nlinks + nbus;
+    if (y.tlb_enable) {
+        const pu_cache_cfg& tc = y.tlb_cache;
+        TlbGeo& T = g->tlb;
+        if (tc.size == 0 || tc.num_ways < 1 || tc.block_size < 1) return pu::set_error(PU_EINVAL, "tlb_enable needs a TLB");
+        if (tc.num_ways > PU_MAX_WAYS) return pu::set_error(PU_ENOTSUP, "at most 64 TLB ways");
+        if (y.page_size < 1) return pu::set_error(PU_EINVAL, "page_size must be >= 1");
+        T.nsets = tc.size / (tc.block_size * tc.num_ways);
+        if (T.nsets < 1) return pu::set_error(PU_EINVAL, "TLB has no sets");
+        T.nways = tc.num_ways;
+        T.page_size = (uint64_t)y.page_size;
+        T.offbits = ilog2((uint64_t)y.page_size);     // Cache::init for TLB_CACHE (cache.cpp:66-69)
+        T.idxbits = ilog2(T.nsets);
+        T.access_time = tc.access_time;
+        T.page_miss_delay = y.page_miss_delay;
+        uint64_t cap = 1ull << 20;
+        if (const char* e = std::getenv("PRIMEUNCORE_PAGE_ENTRIES")) cap = std::strtoull(e, nullptr, 10);
+        uint64_t p2 = 64;
+        while (p2 < cap && p2 < (1ull << 32)) p2 <<= 1;
+        T.pages_cap = p2;
+    }
     for (int l = 0; l < y.num_levels; l++)
         if (g->lv[l].has_bus) g->lv[l].bus_q0 += g->nlinks;
 
@@ -161,19 +181,30 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
         L.off_alive = lay.take((uint64_t)L.ncaches * 4);
         L.off_cnt = lay.take((uint64_t)L.ncaches * 32);
     }
-    uint64_t dlines = (uint64_t)N * D.nsets * D.nways;
+    // the bus system has no directory lines (its report still prints the
+    // directory block, from counters that stay 0)
+    uint64_t dlines = bus_sys ? 0 : (uint64_t)N * D.nsets * D.nways;
     D.off_line = lay.take(dlines * sizeof(DirLine));
     // sharer sets of more than 4 LLCs live in pool bitmaps: one entry per 64
     // directory lines by default (PRIMEUNCORE_POOL_ENTRIES overrides); running
     // out stops the replica with PU_ERRF_POOL rather than diverge
-    uint64_t pool = dlines / 64 < 64 ? 64 : dlines / 64;
-    if (const char* e = std::getenv("PRIMEUNCORE_POOL_ENTRIES")) pool = std::strtoull(e, nullptr, 10);
+    uint64_t pool = bus_sys ? 0 : (dlines / 64 < 64 ? 64 : dlines / 64);
+    if (const char* e = std::getenv("PRIMEUNCORE_POOL_ENTRIES"); e && !bus_sys) pool = std::strtoull(e, nullptr, 10);
     if (pool > (1ull << 30)) pool = 1ull << 30;
     D.pool_entries = (int32_t)pool;
     D.off_pool = lay.take(pool * (uint64_t)D.nwords * 8);
     D.off_pool_free = lay.take(pool * 4);
     D.off_alive = lay.take((uint64_t)N * 4);
     D.off_cnt = lay.take((uint64_t)N * 32);
+    if (y.tlb_enable) {
+        TlbGeo& T = g->tlb;
+        const uint64_t tl = (uint64_t)y.num_cores * T.nsets * T.nways;
+        T.off_meta = lay.take(tl * sizeof(LineMeta));
+        T.off_ts = lay.take(tl * sizeof(int64_t));
+        T.off_ppage = lay.take(tl * sizeof(uint64_t));
+        T.off_cnt = lay.take((uint64_t)y.num_cores * 32);
+        T.off_pages = lay.take(T.pages_cap * sizeof(PageEnt));
+    }
     g->off_qhdr = lay.take((uint64_t)g->nqueues * sizeof(QueueHdr));
     g->off_qring = lay.take((uint64_t)g->nqueues * PU_QRING * sizeof(QueueSlot));
     g->off_stats = lay.take(sizeof(EngineStats));
@@ -254,12 +285,17 @@ int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const 
 }
 
 // Copies replica r's engine-side counters.
-int read_replica(pu_handle* h, int r, EngineStats* es, std::vector<uint64_t> cnt[PU_MAX_LEVELS + 1],
-                 std::vector<uint32_t> alive[PU_MAX_LEVELS + 1]) {
+int read_replica(pu_handle* h, int r, EngineStats* es, std::vector<uint64_t> cnt[PU_MAX_LEVELS + 2],
+                 std::vector<uint32_t> alive[PU_MAX_LEVELS + 2]) {
     const Geo& g = h->geo;
     char* base = h->arena + (size_t)r * g.replica_bytes;
     HIP_TRY(hipStreamSynchronize(h->stream), PU_EIO);
     HIP_TRY(hipMemcpy(es, base + g.off_stats, sizeof(EngineStats), hipMemcpyDeviceToHost), PU_EIO);
+    // [num_levels + 1]: per-core TLB counters (ins, miss, evict, wb)
+    cnt[g.num_levels + 1].assign(g.tlb_enable ? (size_t)g.num_cores * 4 : 0, 0);
+    if (g.tlb_enable)
+        HIP_TRY(hipMemcpy(cnt[g.num_levels + 1].data(), base + g.tlb.off_cnt, (size_t)g.num_cores * 32,
+                          hipMemcpyDeviceToHost), PU_EIO);
     for (int l = 0; l <= g.num_levels; l++) {
         bool dir = l == g.num_levels;
         size_t nc = dir ? (size_t)g.N : (size_t)g.lv[l].ncaches;
@@ -270,6 +306,18 @@ int read_replica(pu_handle* h, int r, EngineStats* es, std::vector<uint64_t> cnt
         HIP_TRY(hipMemcpy(cnt[l].data(), base + oc, nc * 32, hipMemcpyDeviceToHost), PU_EIO);
         HIP_TRY(hipMemcpy(alive[l].data(), base + oa, nc * 4, hipMemcpyDeviceToHost), PU_EIO);
     }
+    return 0;
+}
+
+// The page table of replica r (empty unless tlb_enable).
+int read_pages(pu_handle* h, int r, std::vector<PageEnt>* out) {
+    const Geo& g = h->geo;
+    out->clear();
+    if (!g.tlb_enable) return 0;
+    out->resize(g.tlb.pages_cap);
+    char* base = h->arena + (size_t)r * g.replica_bytes;
+    HIP_TRY(hipMemcpy(out->data(), base + g.tlb.off_pages, g.tlb.pages_cap * sizeof(PageEnt), hipMemcpyDeviceToHost),
+            PU_EIO);
     return 0;
 }
 
@@ -421,6 +469,11 @@ int pu_access(pu_handle* h, int core_id, int prog_id, int mem_type, uint64_t* ad
     int32_t d = 0;
     int rc = pu_access_batch(h, 0, &r, 1, &d);
     if (rc) return rc;
+    if (h->geo.tlb_enable) {    // InsMem::addr_dmem now holds the physical address (system.cpp:916)
+        RunState rs;
+        HIP_TRY(hipMemcpy(&rs, h->arena + h->geo.off_run, sizeof(rs), hipMemcpyDeviceToHost), PU_EIO);
+        *addr = rs.last_addr;
+    }
     return d;
 }
 
@@ -465,8 +518,8 @@ int pu_stats_get(pu_handle* h, int replica, pu_stats* out) {
     if (!h || !out) return pu::set_error(PU_EINVAL, "bad arguments");
     if (replica < 0 || replica >= h->R) return pu::set_error(PU_ERANGE, "replica out of range");
     EngineStats es;
-    std::vector<uint64_t> cnt[PU_MAX_LEVELS + 1];
-    std::vector<uint32_t> alive[PU_MAX_LEVELS + 1];
+    std::vector<uint64_t> cnt[PU_MAX_LEVELS + 2];
+    std::vector<uint32_t> alive[PU_MAX_LEVELS + 2];
     int rc = read_replica(h, replica, &es, cnt, alive);
     if (rc) return rc;
     std::memset(out, 0, sizeof(*out));
@@ -491,6 +544,17 @@ int pu_stats_get(pu_handle* h, int replica, pu_stats* out) {
         if (l == h->geo.num_levels) out->directory = a;
         else out->level[l] = a;
     }
+    {
+        const auto& tc = cnt[h->geo.num_levels + 1];
+        pu_level_stats t{0, 0, 0, 0};
+        for (size_t i = 0; i + 3 < tc.size(); i += 4) {
+            t.ins += tc[i];
+            t.miss += tc[i + 1];
+            t.evict += tc[i + 2];
+            t.wb += tc[i + 3];
+        }
+        out->tlb = t;
+    }
     out->link_flits = es.link_flits;
     out->mg1_calls = es.mg1_calls;
     out->lockdown_calls = es.lockdown_calls;
@@ -507,8 +571,8 @@ long pu_report(pu_handle* h, int replica, int include_time, char* buf, size_t ca
     if (!h) return pu::set_error(PU_EINVAL, "null handle");
     if (replica < 0 || replica >= h->R) return pu::set_error(PU_ERANGE, "replica out of range");
     EngineStats es;
-    std::vector<uint64_t> cnt[PU_MAX_LEVELS + 1];
-    std::vector<uint32_t> alive[PU_MAX_LEVELS + 1];
+    std::vector<uint64_t> cnt[PU_MAX_LEVELS + 2];
+    std::vector<uint32_t> alive[PU_MAX_LEVELS + 2];
     int rc = read_replica(h, replica, &es, cnt, alive);
     if (rc) return rc;
     const Geo& g = h->geo;
@@ -555,6 +619,39 @@ long pu_report(pu_handle* h, int replica, int include_time, char* buf, size_t ca
         o << std::endl;
     }
     o << std::endl;
+    if (g.tlb_enable) {
+        // system.cpp:990-1014 ("replaced" is never accumulated, Q16)
+        const auto& tc = cnt[g.num_levels + 1];
+        uint64_t ins = 0, miss = 0;
+        for (size_t i = 0; i + 3 < tc.size(); i += 4) {
+            ins += tc[i];
+            miss += tc[i + 1];
+        }
+        double miss_rate = (double)miss / (double)ins;
+        o << "TLB Cache" << "===========================================================\n";
+        o << "Simulation results for " << y.tlb_cache.size << " Bytes " << y.tlb_cache.num_ways
+          << "-way set associative cache model:\n";
+        o << "The total # of TLB access instructions: " << ins << std::endl;
+        o << "The # of cache-missed instructions: " << miss << std::endl;
+        o << "The # of replaced instructions: " << 0 << std::endl;
+        o << "The cache miss rate: " << 100 * miss_rate << "%" << std::endl;
+        o << "=================================================================\n\n";
+        if (y.verbose_report) {
+            // PageTable::report (page_table.cpp:79-87): std::map order of (prog, vpage)
+            std::vector<PageEnt> tab;
+            int prc = read_pages(h, replica, &tab);
+            if (prc) return prc;
+            std::vector<std::pair<std::pair<int, uint64_t>, uint64_t>> pages;
+            for (const PageEnt& e : tab)
+                if (e.used) pages.push_back({{e.prog, e.vpage}, e.ppage});
+            std::sort(pages.begin(), pages.end());
+            o << "Page translation:\n";
+            o << "Total # of pages: " << pages.size() << std::endl;
+            for (const auto& kv : pages)
+                o << std::dec << "(proc ID: " << kv.first.first << " ,vpage Num: " << std::hex << kv.first.second
+                  << ") => " << "ppage Num: " << kv.second << std::dec << std::endl;
+        }
+    }
     o << std::endl;
     o << "Total delay caused by bus contention: " << es.total_bus_contention << " cycles\n";
     o << "Total # of broadcast: " << (int)es.total_num_broadcast << "\n\n";
@@ -618,6 +715,17 @@ long pu_report(pu_handle* h, int replica, int include_time, char* buf, size_t ca
             if (da[j] && dc[j * 4] > 0) {
                 o << "Report for directory cache " << j << std::endl;
                 cache_report(o, y.directory_cache.size, y.directory_cache.num_ways, &dc[j * 4]);
+            }
+        }
+        if (g.tlb_enable) {
+            o << "****************************************************" << std::endl;
+            o << "Statistics for each TLB cache with non-zero accesses" << std::endl;
+            const auto& tc = cnt[g.num_levels + 1];
+            for (int j = 0; j < g.num_cores; j++) {
+                if (tc[(size_t)j * 4] > 0) {
+                    o << "Report for tlb cache " << j << std::endl;
+                    cache_report(o, y.tlb_cache.size, y.tlb_cache.num_ways, &tc[(size_t)j * 4]);
+                }
             }
         }
     }

@@ -59,6 +59,10 @@ def report_stats(text: str) -> dict:
     m = re.search(r"Directory Cache=+\n.*?\nThe total # of memory instructions: (\d+)\n"
                   r"The # of cache-missed instructions: (\d+)\nThe # of replaced instructions: (\d+)", text, re.S)
     out["directory_ins"], out["directory_miss"], out["directory_evict"] = map(int, m.groups())
+    m = re.search(r"TLB Cache=+\n.*?\nThe total # of TLB access instructions: (\d+)\n"
+                  r"The # of cache-missed instructions: (\d+)", text, re.S)
+    if m:                                   # system.cpp:990-1009 (tlb_enable)
+        out["tlb_ins"], out["tlb_miss"] = map(int, m.groups())
     return out
 
 

@@ -50,8 +50,8 @@ def test_no_gpu_fails_loudly():
 
 
 @pytest.mark.parametrize("mutate,msg", [
-    (lambda s: s["system"].update(tlb_enable=1), "tlb_enable"),
-    (lambda s: s["system"].update(sys_type=1), "sys_type"),
+    (lambda s: s["system"].update(tlb_enable=1, tlb_cache=dict(s["system"]["tlb_cache"], size=0)), "TLB"),
+    (lambda s: s["system"].update(sys_type=2), "sys_type"),
     (lambda s: s["system"]["cache"][0].update(share=2), "L1 share"),
     (lambda s: s["system"]["network"].update(link_delay=0), "link_delay"),
     (lambda s: s["system"]["directory_cache"].update(size=0), "directory"),
@@ -66,6 +66,20 @@ def test_config_validation_before_device(mutate, msg):
     h = lib().pu_create(C.byref(cfg), 1, 0)
     assert not h
     assert msg in P.uncore.last_error()
+
+
+@pytest.mark.skipif(_gpu_present(), reason="checks the no-GPU path")
+@pytest.mark.parametrize("mutate", [lambda s: s["system"].update(tlb_enable=1),
+                                    lambda s: s["system"].update(sys_type=1),
+                                    lambda s: s["system"].update(sys_type=1, tlb_enable=1)])
+def test_bus_and_tlb_configs_are_accepted(mutate):
+    """sys_type=1 (mesi_bus) and tlb_enable=1 pass validation: creation only stops at the missing device."""
+    sim = CF.preset("C1")
+    mutate(sim)
+    cfg = P.config_from_dict(sim)
+    h = lib().pu_create(C.byref(cfg), 1, 0)
+    assert not h
+    assert "no HIP device" in P.uncore.last_error()
 
 
 def test_stream_api_errors():

@@ -117,6 +117,30 @@ def cases() -> dict:
     c["verbose"] = (_c1_shape(16, verbose_report=1), S(A.PU_STREAM_UNIFORM_HOTSPOT, 16, seed=17, num_quanta=1))
     c["verbose_l2"] = (dict(_l2_shared(16), **{}), S(A.PU_STREAM_UNIFORM_HOTSPOT, 16, seed=18, num_quanta=1))
     c["verbose_l2"][0]["system"]["verbose_report"] = 1
+    # TLB + first-touch page table (system.cpp:897-918, page_table.cpp:56-72):
+    # config_prime's 64-entry fully associative TLB, 4 KB pages, several programs
+    c["tlb_c1"] = (_c1_shape(16, tlb_enable=1), S(A.PU_STREAM_MULTIPROGRAM, 16, seed=21, num_quanta=2, num_progs=2))
+    c["tlb_verbose"] = (_c1_shape(16, tlb_enable=1, verbose_report=1),
+                        S(A.PU_STREAM_MULTIPROGRAM, 16, seed=22, num_quanta=1, num_progs=4))
+    c["tlb_c3"] = (CF.preset("C3", tlb_enable=1), S(A.PU_STREAM_MULTIPROGRAM, 256, seed=23, num_quanta=1,
+                                                    num_progs=4, max_requests=20000))
+    tlb_sa = _c1_shape(16, tlb_enable=1, page_size=1024, page_miss_delay=150)
+    tlb_sa["system"]["tlb_cache"] = {"level": 0, "share": 1, "access_time": 1, "size": 32, "block_size": 1,
+                                     "num_ways": 4}
+    c["tlb_setassoc"] = (tlb_sa, S(A.PU_STREAM_SHARED_UNIFORM, 16, seed=28, num_quanta=2))
+    # snoopy bus MESI (sys_type=1, system.cpp:224-368)
+    c["bus_c1"] = (_c1_shape(16, sys_type=1), S(A.PU_STREAM_UNIFORM_HOTSPOT, 16, seed=24, num_quanta=2))
+    bl2 = _l2_shared(64)
+    bl2["system"]["sys_type"] = 1
+    c["bus_l2_shared"] = (bl2, S(A.PU_STREAM_MULTIPROGRAM, 64, seed=25, num_quanta=1, num_progs=2,
+                                 max_requests=20000))
+    b3 = _three_level(64)
+    b3["system"]["sys_type"] = 1
+    c["bus_three_level"] = (b3, S(A.PU_STREAM_SHARED_UNIFORM, 64, seed=26, num_quanta=1, max_requests=20000))
+    c["bus_tlb_verbose"] = (_c1_shape(16, sys_type=1, tlb_enable=1, verbose_report=1),
+                            S(A.PU_STREAM_MULTIPROGRAM, 16, seed=27, num_quanta=1, num_progs=2))
+    c["bus_c2"] = (CF.preset("C2", sys_type=1), S(A.PU_STREAM_SHARED_UNIFORM, 64, seed=29, num_quanta=1,
+                                                  max_requests=20000))
     return c
 
 
