@@ -303,6 +303,36 @@ int pu_trace_write(const char* path, const pu_req* reqs, size_t n,
                    const int32_t* thread_prog, const int32_t* thread_id, int num_threads);
 
 /* ------------------------------------------------------------------------
+ * MsgMem message logs: the receive stream of the
+ * reference's uncore server, message by message as prime.cpp:53 gets it
+ * (MPI source rank + the MsgMem records of reference src/common.h:49-59, 24 B
+ * each).  File: "PRIMEMSG" | u32 1 | u32 24, then per message
+ * i32 source | i32 n_records | records.  Replay applies prime.cpp:55-137:
+ * NEW_THREAD -> allocCore, THREAD_FINISHING -> deallocCore, MEM_REQUESTS ->
+ * getCoreId + requests 1..addr_dmem-1 with prog_id = source; other control
+ * messages have no uncore effect, PROGRAM_EXITING ends the log.
+ * ---------------------------------------------------------------------- */
+typedef struct pu_msglog pu_msglog;
+/* Open for replay; num_cores sizes the log's own ThreadSched (used when
+ * pu_msglog_next gets h == NULL). */
+pu_msglog* pu_msglog_open(const char* path, int num_cores);
+/* Next requests (<= cap) in receive order, core ids resolved through h's
+ * ThreadSched (h may be NULL: the log's own).  batch_start marks each
+ * message's first request.  Returns the count, 0 at the end, or PU_E*. */
+int64_t    pu_msglog_next(pu_msglog* L, pu_handle* h, pu_req* out, size_t cap);
+int64_t    pu_msglog_messages(const pu_msglog* L);
+/* Capture: create a log and append messages as received (the three fwrite
+ * calls a prime.cpp build would add after MPI_Recv). */
+pu_msglog* pu_msglog_create(const char* path);
+int        pu_msglog_append(pu_msglog* L, int32_t source, const void* records, int32_t n_records);
+int        pu_msglog_close(pu_msglog* L);
+/* A canonical-order request stream written as the log its cores would have
+ * sent (NEW_THREAD per thread, one MEM_REQUESTS message per batch). */
+int pu_msglog_from_requests(const char* path, const pu_req* reqs, size_t n, const int32_t* thread_prog,
+                            const int32_t* thread_id, int num_threads, const int32_t* core_thread,
+                            int num_cores);
+
+/* ------------------------------------------------------------------------
  * Unit hooks: run one engine component alone on the GPU (one wavefront), for
  * the component-level parity tests.
  * ---------------------------------------------------------------------- */

@@ -6,7 +6,8 @@ schema (`config`) and the ctypes ABI definitions (`_abi`).
 """
 from . import _abi, config  # noqa: F401
 from .uncore import (InsMem, StreamSet, StreamSpec, UncoreError, UncoreManager, config_from_dict,  # noqa: F401
-                     generate_stream, load_config, parse_config, stream_threads)
+                     generate_stream, load_config, msglog_from_stream, msglog_read, parse_config,
+                     stream_threads, MsgLogWriter)
 
 __all__ = ["InsMem", "StreamSet", "StreamSpec", "UncoreError", "UncoreManager", "config_from_dict", "generate_stream",
-           "load_config", "parse_config", "stream_threads"]
+           "load_config", "msglog_from_stream", "msglog_read", "MsgLogWriter", "parse_config", "stream_threads"]

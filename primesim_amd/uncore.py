@@ -74,6 +74,14 @@ def lib() -> C.CDLL:
         "pu_stream_next": (C.c_int64, [C.c_void_p, C.c_void_p, C.c_size_t]),
         "pu_stream_position": (C.c_int64, [C.c_void_p]),
         "pu_stream_next_many": (C.c_int64, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.c_size_t, C.c_int]),
+        "pu_msglog_open": (C.c_void_p, [C.c_char_p, C.c_int]),
+        "pu_msglog_next": (C.c_int64, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+        "pu_msglog_messages": (C.c_int64, [C.c_void_p]),
+        "pu_msglog_create": (C.c_void_p, [C.c_char_p]),
+        "pu_msglog_append": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]),
+        "pu_msglog_close": (C.c_int, [C.c_void_p]),
+        "pu_msglog_from_requests": (C.c_int, [C.c_char_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int,
+                                              C.c_void_p, C.c_int]),
         "pu_trace_write": (C.c_int, [C.c_char_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int]),
         "pu_unit_queue_run": (C.c_int, [C.c_uint64, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
                                         P(C.c_uint64), C.c_int]),
@@ -197,6 +205,69 @@ class StreamSet:
             self.close()
         except Exception:
             pass
+
+
+# ---------------------------------------------------------------- MsgMem logs
+MSGMEM_DTYPE = np.dtype([("mem_type", np.uint8), ("_pad", np.uint8, 3), ("mem_size", np.int32),
+                         ("addr_dmem", np.uint64), ("timer", np.int64)])   # reference common.h:49-59
+assert MSGMEM_DTYPE.itemsize == 24
+MSG_MEM_REQUESTS, MSG_PROCESS_STARTING, MSG_PROCESS_FINISHING = 0, -3, -1
+MSG_BARRIER, MSG_NEW_THREAD, MSG_THREAD_FINISHING, MSG_PROGRAM_EXITING = -2, -4, -8, -5
+
+
+def msglog_from_stream(path: str, reqs: np.ndarray, spec: "StreamSpec") -> None:
+    """Write a synthetic stream as the MsgMem message log its cores would have sent."""
+    threads = stream_threads(spec)
+    tp = np.array([t[0] for t in threads], np.int32)
+    ti = np.array([t[1] for t in threads], np.int32)
+    ct = np.arange(spec.num_cores, dtype=np.int32)
+    reqs = np.ascontiguousarray(reqs, dtype=A.REQ_DTYPE)
+    rc = lib().pu_msglog_from_requests(path.encode(), reqs.ctypes.data, len(reqs), tp.ctypes.data, ti.ctypes.data,
+                                       len(threads), ct.ctypes.data, spec.num_cores)
+    if rc != 0:
+        raise UncoreError(f"msglog: {last_error()}")
+
+
+class MsgLogWriter:
+    """Capture side: append messages exactly as prime.cpp:53 receives them."""
+
+    def __init__(self, path: str):
+        self._h = lib().pu_msglog_create(path.encode())
+        if not self._h:
+            raise UncoreError(f"msglog: {last_error()}")
+
+    def append(self, source: int, records: np.ndarray) -> None:
+        records = np.ascontiguousarray(records, dtype=MSGMEM_DTYPE)
+        if lib().pu_msglog_append(self._h, source, records.ctypes.data, len(records)) != 0:
+            raise UncoreError(f"msglog: {last_error()}")
+
+    def close(self) -> None:
+        if self._h:
+            lib().pu_msglog_close(self._h)
+            self._h = None
+
+
+def msglog_read(path: str, um: "UncoreManager | None" = None, num_cores: int = 0,
+                chunk: int = 1 << 16) -> np.ndarray:
+    """Replay a MsgMem log into requests (prime.cpp:55-137 semantics), resolving
+    core ids through um's ThreadSched (or the log's own over num_cores cores)."""
+    L = lib().pu_msglog_open(path.encode(), num_cores)
+    if not L:
+        raise UncoreError(f"msglog: {last_error()}")
+    parts = []
+    try:
+        h = um._handle() if um is not None else None
+        while True:
+            buf = np.zeros(chunk, dtype=A.REQ_DTYPE)
+            n = lib().pu_msglog_next(L, h, buf.ctypes.data, chunk)
+            if n < 0:
+                raise UncoreError(f"msglog: {last_error()}")
+            if n == 0:
+                break
+            parts.append(buf[:n])
+    finally:
+        lib().pu_msglog_close(L)
+    return np.concatenate(parts) if parts else np.zeros(0, dtype=A.REQ_DTYPE)
 
 
 def stream_threads(spec: StreamSpec) -> list[tuple[int, int]]:
