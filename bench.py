@@ -7,16 +7,22 @@ DRAM 120 cycles; synthetic stream: 80% uniform over 2^20 lines + 20% over a
 64-line hotspot, 25% writes, 1-4-cycle gaps, 1000-cycle barriers,
 100-request messages, canonical order.
 
-One "step" = every replica on this GPU advances its own request stream by
---chunk (40,960) requests in one engine launch (the hot path: prime.cpp's
-message loop over System::access).  A quantum of the C4 stream is ~409,600
-requests (1024 cores x ~400 requests per 1000-cycle quantum), so the default
-10 warmup steps run the first quantum (every core active; cold caches and empty
-link histories) untimed and the 10 timed steps run the second quantum.  A replica is one complete, independent 1024-core uncore
-(its own seed); the engine runs one replica per wavefront and many replicas
-per GPU, because a single uncore is a strictly sequential fold.
-`value` = all requests processed by all ranks / max-over-ranks wall time of the
-K timed steps, with the requests already resident in HBM.
+Every replica on this GPU first runs the first quantum of its own request
+stream untimed, in --warmup fixed steps of --chunk (40,960) requests (a C4
+quantum is ~409,600 requests: 1024 cores x ~400 requests per 1000-cycle
+quantum, so every core is active; cold caches and empty link histories).  The
+requests of the next --steps x --chunk are then made resident in HBM and each
+timed "step" is one engine launch (the hot path: prime.cpp's message loop over
+System::access) in which every replica continues its own stream for a
+--slice-ms wall-time slice, stopping only between requests
+(pu_run_device_sliced).  Replicas differ several-fold in cost per request (link
+histories, tree-vs-M/G/1 mix), so a fixed number of requests per replica per
+launch would leave most waves idle behind the slowest (measured 26% busy); the
+slice keeps every wave simulating.  A replica is one complete, independent
+1024-core uncore (its own seed); the engine runs one replica per wavefront and
+many replicas per GPU, because a single uncore is a strictly sequential fold
+(DESIGN.md).  `value` = all requests processed by all ranks / max-over-ranks
+wall time of the K timed steps.  --slice-ms 0 gives fixed --chunk steps.
 
 Rank 0 also times the reference's own CPU uncore (oracle/_ref, compiled from
 /root/reference in the build container) — or, if that library is absent, the
@@ -330,7 +336,7 @@ def main() -> None:
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": "uncore_kernel<1>",
+                "kernel": "uncore_kernel<1, true>" if args.slice_ms > 0 else "uncore_kernel<1, true> (no budget)",
                 "avg_launch_ms": avg_ms,
                 "alg_bytes_per_launch": bytes_per_launch,
             },

@@ -1608,12 +1608,18 @@ __device__ __forceinline__ void stats_init() {
 // ever stops between requests, so its stream continues exactly in the next
 // launch; the slice keeps every wave busy instead of waiting for the slowest
 // replica of a fixed-size step.
-template <int NL>
+// SLICED is a separate instantiation so profiles list the time-sliced launches
+// (uncore_kernel<NL, true>) apart from fixed-range ones.
+template <int NL, bool SLICED>
 __global__ __launch_bounds__(64) void uncore_kernel(const Geo* __restrict__ g, char* __restrict__ arena,
                                                     int replica0, const pu_req* __restrict__ reqs,
                                                     const uint64_t* __restrict__ off,
                                                     int32_t* __restrict__ delays, uint64_t* __restrict__ pos,
                                                     uint64_t budget_ticks) {
+    if constexpr (!SLICED) {
+        pos = nullptr;
+        budget_ticks = 0;
+    }
     const uint64_t wave_t0 = __builtin_amdgcn_s_memrealtime();
     Engine<NL> e;
     e.g = g;
@@ -1798,11 +1804,17 @@ extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, i
                                 const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
                                 uint64_t budget_ticks, hipStream_t stream) {
     dim3 grid((unsigned)nblocks), block(64);
+#define PU_LAUNCH(L)                                                                                              \
+    if (pos) hipLaunchKernelGGL((uncore_kernel<L, true>), grid, block, 0, stream, d_geo, arena, replica0, reqs, off, \
+                                delays, pos, budget_ticks);                                                      \
+    else hipLaunchKernelGGL((uncore_kernel<L, false>), grid, block, 0, stream, d_geo, arena, replica0, reqs, off,   \
+                            delays, pos, budget_ticks);
     switch (num_levels) {
-        case 1: hipLaunchKernelGGL(uncore_kernel<1>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays, pos, budget_ticks); break;
-        case 2: hipLaunchKernelGGL(uncore_kernel<2>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays, pos, budget_ticks); break;
-        case 3: hipLaunchKernelGGL(uncore_kernel<3>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays, pos, budget_ticks); break;
-        case 4: hipLaunchKernelGGL(uncore_kernel<4>, grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays, pos, budget_ticks); break;
+        case 1: PU_LAUNCH(1); break;
+        case 2: PU_LAUNCH(2); break;
+        case 3: PU_LAUNCH(3); break;
+        case 4: PU_LAUNCH(4); break;
+#undef PU_LAUNCH
         default: return PU_EINVAL;
     }
     return hipGetLastError() == hipSuccess ? 0 : PU_EIO;

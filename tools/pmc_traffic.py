@@ -26,7 +26,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "uncore_kernel"
+KERNEL = "uncore_kernel<1, true>"   # the timed (time-sliced) launches of bench.py
 
 
 def run(cmd, log):
