@@ -240,6 +240,49 @@ __device__ __forceinline__ uint64_t scan_incl_u64(uint64_t v) {
     return v;
 }
 
+// Cache::lru (cache.cpp:167-179): the way with the smallest timestamp, lowest
+// way on ties, over lanes 0..nways-1 (other lanes pass INT64_MAX / way 64).
+// Up to 16 ways the butterfly stays inside a DPP row (quad_perm xor 1, xor 2,
+// row_half_mirror, row_mirror: a few cycles per step); wider sets fall back to
+// cross-row shuffles.  The (ts, way) minimum is order-independent.
+template <int CTRL>
+__device__ __forceinline__ void lru_step_dpp(int64_t& bt, int& bw) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)bt, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)((uint64_t)bt >> 32), CTRL, 0xF, 0xF,
+                                                              false);
+    const int ow = __builtin_amdgcn_update_dpp(0, bw, CTRL, 0xF, 0xF, false);
+    const int64_t ot = (int64_t)(((uint64_t)hi << 32) | lo);
+    if (ot < bt || (ot == bt && ow < bw)) {
+        bt = ot;
+        bw = ow;
+    }
+}
+__device__ __forceinline__ int lru_way(int64_t bt, int bw, uint64_t nways) {
+    if (nways <= 16) {
+        lru_step_dpp<0xB1>(bt, bw);      // quad_perm [1,0,3,2]
+        lru_step_dpp<0x4E>(bt, bw);      // quad_perm [2,3,0,1]
+        lru_step_dpp<0x141>(bt, bw);     // row_half_mirror
+        if (nways > 8) lru_step_dpp<0x140>(bt, bw);   // row_mirror
+        return (int)__builtin_amdgcn_readfirstlane(bw);
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        int64_t ot = (int64_t)shfl64((uint64_t)bt, (int)threadIdx.x ^ o);
+        int ow = __shfl(bw, (int)threadIdx.x ^ o, 64);
+        if (ot < bt || (ot == bt && ow < bw)) {
+            bt = ot;
+            bw = ow;
+        }
+    }
+    return (int)__builtin_amdgcn_readfirstlane(bw);
+}
+
+// Cache::addrParse's set index (cache.cpp:145-152): a mask when the set count
+// is a power of two (a runtime-uniform branch), the general modulo otherwise.
+__device__ __forceinline__ uint64_t set_index(uint64_t addr, int offbits, uint64_t nsets) {
+    const uint64_t x = addr >> offbits;
+    return (nsets & (nsets - 1)) == 0 ? (x & (nsets - 1)) : x % nsets;
+}
+
 // computeQueueDelay's outcome for interval [f, s] if the search stops there
 // (queue_model_history_tree.cpp:74-106): op 1 second<-t, 2 first<-t+d+p,
 // 3 remove, 4 split; returns the delay d.
@@ -784,7 +827,7 @@ struct Engine {
     __device__ __forceinline__ void set_load(SetView& v, const LineMeta* meta, const int64_t* ts,
                                              uint64_t nsets, uint64_t nways, int offbits, int idxbits,
                                              uint64_t cache_index, uint64_t addr) const {
-        v.set = (addr >> offbits) % nsets;
+        v.set = set_index(addr, offbits, nsets);
         v.tag = addr >> (offbits + idxbits);
         v.line0 = (cache_index * nsets + v.set) * nways;
         if ((uint64_t)ln < nways) {
@@ -817,17 +860,7 @@ struct Engine {
             *old_addr = 0;
             *old_prog = 0;
         } else {
-            int64_t bt = v.mts;
-            int bw = (uint64_t)ln < nways ? ln : 64;
-            for (int o = 32; o >= 1; o >>= 1) {
-                int64_t ot = (int64_t)shfl64((uint64_t)bt, ln ^ o);
-                int ow = __shfl(bw, ln ^ o, 64);
-                if (ot < bt || (ot == bt && ow < bw)) {
-                    bt = ot;
-                    bw = ow;
-                }
-            }
-            way = (int)uni32((uint32_t)bw);
+            way = lru_way(v.mts, (uint64_t)ln < nways ? ln : 64, nways);
             *old_state = rl32(v.mst, way);
             *old_addr = (v.set << offbits) | (rl64(v.mtag, way) << (offbits + idxbits));
             *old_prog = (int)rl32((uint32_t)v.mid, way);
@@ -1071,7 +1104,7 @@ struct Engine {
         const int blk = (int)g->lv[last].block;
         DirLine* lines = at<DirLine>(D.off_line);
         if (ln == (home & 63)) at<uint32_t>(D.off_alive)[home] = 1u;   // home_stat[home] = 1
-        const uint64_t set = (r.addr >> D.offbits) % D.nsets;
+        const uint64_t set = set_index(r.addr, D.offbits, D.nsets);
         const uint64_t tag = r.addr >> (D.offbits + D.idxbits);
         const uint64_t line0 = ((uint64_t)home * D.nsets + set) * D.nways;
         const bool mine = (uint64_t)ln < D.nways;
@@ -1105,17 +1138,7 @@ struct Engine {
             if (inv) {
                 way = (int)__builtin_ctzll(inv);
             } else {
-                int64_t bt = m.ts;
-                int bw = mine ? ln : 64;
-                for (int o = 32; o >= 1; o >>= 1) {
-                    int64_t ot = (int64_t)shfl64((uint64_t)bt, ln ^ o);
-                    int ow = __shfl(bw, ln ^ o, 64);
-                    if (ot < bt || (ot == bt && ow < bw)) {
-                        bt = ot;
-                        bw = ow;
-                    }
-                }
-                way = (int)uni32((uint32_t)bw);
+                way = lru_way(m.ts, mine ? ln : 64, D.nways);
                 old_st = rl32(m.state, way);
                 old_addr = (set << D.offbits) | (rl64(m.tag, way) << (D.offbits + D.idxbits));
                 old_prog = (int)rl32((uint32_t)m.id, way);
@@ -1219,9 +1242,9 @@ struct Engine {
 
     __device__ __forceinline__ int home_of(uint64_t addr) const {
         // System::allocHomeId (system.cpp:921-936)
-        int hb = (int)((addr >> g->home_offbits) % (uint64_t)(1 << g->home_mask_bits));
+        int hb = (int)((addr >> g->home_offbits) & (((uint64_t)1 << g->home_mask_bits) - 1));
         if (hb < g->N) return hb;
-        return hb % (1 << (g->home_mask_bits - 1));
+        return hb & ((1 << (g->home_mask_bits - 1)) - 1);
     }
 
     // ------------------------------------------------------------ directory MESI walk
@@ -1360,7 +1383,7 @@ struct Engine {
         constexpr int last = NL - 1;
         const LevelGeo& L = g->lv[last];
         LineMeta* meta = at<LineMeta>(L.off_meta);
-        const uint64_t set = (r.addr >> L.offbits) % L.nsets;
+        const uint64_t set = set_index(r.addr, L.offbits, L.nsets);
         const uint64_t tag = r.addr >> (L.offbits + L.idxbits);
         bool any = false;
         for (int base = 0; base < L.ncaches; base += 64) {
