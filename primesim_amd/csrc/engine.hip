@@ -315,9 +315,6 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
     const uint32_t jh = ((uint32_t)ln + 64 - head) & (PU_QRING - 1);
     const bool pl = jl < cnt && ((v.lf <= t && tp <= v.ls) || (t < v.lf && v.ls - v.lf >= p));
     const bool ph = jh < cnt && ((v.hf <= t && tp <= v.hs) || (t < v.hf && v.hs - v.hf >= p));
-    uint32_t opl, oph;
-    const uint64_t dl_ = tree_case(v.lf, v.ls, t, p, minp, opl);
-    const uint64_t dh_ = tree_case(v.hf, v.hs, t, p, minp, oph);
     uint64_t ml = ballot(pl), mh = ballot(ph);
     // logical order: rotate the 128-bit hit mask right by head
     const uint32_t hsh = head & 63;
@@ -338,9 +335,12 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
     const uint32_t slot = (head + k) & (PU_QRING - 1);
     PROF_ADD(PF_T_SEARCH, p_s);
     PROF_T(p_d);
+    // the outcome for the found interval only, on the scalar unit
     const bool hi_half = slot >= 64;
-    const uint32_t op = rl32(hi_half ? oph : opl, (int)(slot & 63));
-    const uint64_t d = rl64(hi_half ? dh_ : dl_, (int)(slot & 63));
+    const uint64_t sf = rl64(hi_half ? v.hf : v.lf, (int)(slot & 63));
+    const uint64_t ss = rl64(hi_half ? v.hs : v.ls, (int)(slot & 63));
+    uint32_t op;
+    const uint64_t d = tree_case(sf, ss, t, p, minp, op);
     // the edit as: slots whose logical index is in [r0, r0+rlen) take their
     // NEXT/PREV neighbour; then first<-fv at logical fi, second<-t at si
     uint32_t r0 = 0, rlen = 0, fi = 0xFFFFFFFFu, si = 0xFFFFFFFFu;
@@ -404,10 +404,8 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
     if (wh) R[ln + 64] = v2u64{hf, hs};
     // the header's copies of the first two interval starts
     const uint32_t s0 = head, s1 = (head + 1) & (PU_QRING - 1);
-    const uint64_t a0 = rl64(lf, (int)(s0 & 63)), b0 = rl64(hf, (int)(s0 & 63));
-    const uint64_t a1 = rl64(lf, (int)(s1 & 63)), b1 = rl64(hf, (int)(s1 & 63));
-    f0n = s0 < 64 ? a0 : b0;
-    f1n = s1 < 64 ? a1 : b1;
+    f0n = rl64(s0 < 64 ? lf : hf, (int)(s0 & 63));
+    f1n = rl64(s1 < 64 ? lf : hf, (int)(s1 & 63));
     PROF_ADD(PF_T_STORE, p_w);
     return d;
 }
@@ -712,7 +710,8 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
             uint32_t head = rl32(vhead, jt), cnt = rl32(vcnt, jt);
             uint64_t f0n, f1n, d;
             RingView v;
-            if (mc && jt == (int)__builtin_ctzll(mc)) {
+            const bool staged = mc && jt == (int)__builtin_ctzll(mc);
+            if (staged) {
                 // predicted: its ring is (being) staged in LDS slot consumed % PF
                 mc &= mc - 1;
                 PROF_T(p_wait);
@@ -720,19 +719,18 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                 PROF_ADD(PF_NWAIT, p_wait);
                 ring_from_lds(consumed % PU_RING_PF, v);
                 consumed++;
-                d = tree_op(c, q, v, head, cnt, tj, (uint64_t)plen, c.link_delay, err, f0n, f1n);
-                PROF_T(p_r);
-                if (mi) {                       // keep PF rings in flight
-                    const int jj = (int)__builtin_ctzll(mi);
-                    mi &= mi - 1;
-                    ring_dma(c, (int)rl32((uint32_t)rq, jj), rl32(vhead, jj), rl32(vcnt, jj), issued % PU_RING_PF);
-                    issued++;
-                }
-                PROF_ADD(PF_T_REFILL, p_r);
             } else {                            // not predicted (arrival pushed past the front)
                 PROF_CNT(PF_DEMAND, 1);
                 ring_load(c, q, head, cnt, v);
-                d = tree_op(c, q, v, head, cnt, tj, (uint64_t)plen, c.link_delay, err, f0n, f1n);
+            }
+            d = tree_op(c, q, v, head, cnt, tj, (uint64_t)plen, c.link_delay, err, f0n, f1n);
+            if (staged && mi) {                 // keep PF rings in flight
+                PROF_T(p_r);
+                const int jj = (int)__builtin_ctzll(mi);
+                mi &= mi - 1;
+                ring_dma(c, (int)rl32((uint32_t)rq, jj), rl32(vhead, jj), rl32(vcnt, jj), issued % PU_RING_PF);
+                issued++;
+                PROF_ADD(PF_T_REFILL, p_r);
             }
             vhead = wl32(vhead, head, jt);
             vcnt = wl32(vcnt, cnt, jt);
@@ -769,14 +767,18 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
     t += c.router;
     t += (uint64_t)(plen - 1);
     const uint64_t dist = (uint64_t)hops;
-    stat_add(SN_ACC, 1);
-    stat_add(SN_TOTAL, t - timer);
-    stat_add(SN_ROUTER, (dist + 1) * c.router);
-    stat_add(SN_LINK, t - timer - (dist + 1) * c.router - (uint64_t)(plen - 1) - c.inject);
-    stat_add(SN_INJECT, c.inject);
-    stat_add(SN_DIST, dist);
-    stat_add(SN_FLITS, dist * (uint64_t)plen);
-    stat_add(SN_MG1, mg1);
+    {   // the eight network counters in one ds_add_u64, lane k adding counter k
+        const uint64_t tot = t - timer, rt = (dist + 1) * c.router;
+        uint64_t sv = ln == SN_ACC ? 1ull : 0ull;
+        sv = ln == SN_DIST ? dist : sv;
+        sv = ln == SN_TOTAL ? tot : sv;
+        sv = ln == SN_ROUTER ? rt : sv;
+        sv = ln == SN_LINK ? tot - rt - (uint64_t)(plen - 1) - c.inject : sv;
+        sv = ln == SN_INJECT ? c.inject : sv;
+        sv = ln == SN_FLITS ? dist * (uint64_t)plen : sv;
+        sv = ln == SN_MG1 ? mg1 : sv;
+        if (ln <= SN_MG1 && ln != SN_DRAM && ln != SN_BUSCONT) atomicAdd(&lds_stat[ln], (unsigned long long)sv);
+    }
     if (err) err_or(err);
     return t - timer;
 }
@@ -1074,9 +1076,12 @@ struct Engine {
             }
             k++;
             int t = pipe;
-            t += (int)transmit(home, p, 0, (uint64_t)(base_t + t));
-            t += inval ? down<last, true>(p, r) : down<last, false>(p, r);
-            t += (int)transmit(p, home, reply_len, (uint64_t)(base_t + t));
+            // home -> p, share/inval below p, p -> home: one transmit site
+#pragma clang loop unroll(disable)
+            for (int back = 0; back < 2; back++) {
+                t += (int)transmit(back ? p : home, back ? home : p, back ? reply_len : 0, (uint64_t)(base_t + t));
+                if (!back) t += inval ? down<last, true>(p, r) : down<last, false>(p, r);
+            }
             if (single) return t;
             mx = t > mx ? t : mx;
             pipe += g->header_flits;
@@ -1341,21 +1346,26 @@ struct Engine {
                 if (is_miss) ret = ns;
             }
         } else {
+            // legs: 0 the write-back to its home (delays discarded, Q3), 1 the
+            // request to its home, 2 the reply; one transmit site and one home
+            // access site serve all of them
             const int req_home = home_of(r.addr);
-            for (int k = tx_wb ? 0 : 1; k < (tx_req ? 2 : 1); k++) {
-                const bool wb = k == 0;
+            int leg = tx_wb ? 0 : (tx_req ? 1 : 3);
+            while (leg < 3) {
+                const bool wb = leg == 0;
                 const int home = wb ? wb_home : req_home;
-                const Req& q = wb ? wb_req : r;
-                const int to_len = wb ? (int)L.block : 0;
-                const int d1 = (int)transmit(cid, home, to_len, (uint64_t)(timer + dly));
+                const int src = leg == 2 ? home : cid, dst = leg == 2 ? cid : home;
+                const int len = wb ? (int)L.block : (leg == 1 ? 0 : req_reply);
+                const int d1 = (int)transmit(src, dst, len, (uint64_t)(timer + dly));
                 if (!wb) dly += d1;
+                if (leg == 2) break;
                 uint32_t hs;
-                const int d2 = access_home(cid, home, q, timer + dly, &hs);
+                const int d2 = access_home(cid, home, wb ? wb_req : r, timer + dly, &hs);
                 if (!wb) {
                     dly += d2;
-                    dly += (int)transmit(home, cid, req_reply, (uint64_t)(timer + dly));
                     if (is_miss) ret = hs;
                 }
+                leg = wb ? (tx_req ? 1 : 3) : 2;
             }
             set_state(v, meta, way, is_miss ? ret : ST_M);
         }
