@@ -175,6 +175,9 @@ typedef struct pu_stats {
                                              raise PRIMEUNCORE_POOL_ENTRIES) */
 #define PU_ERRF_PAGES        (1ull << 6)  /* page table 3/4 full (engine limit;
                                              raise PRIMEUNCORE_PAGE_ENTRIES) */
+#define PU_ERRF_PROG         (1ull << 7)  /* prog_id outside [0, 1024) in a directory
+                                             system (engine limit: packed directory
+                                             lines; the replica stops at that request) */
 
 /* ------------------------------------------------------------------------
  * Engine lifetime and the hot path.

@@ -26,6 +26,7 @@ PU_ERRF_QUEUE = 1 << 3
 PU_ERRF_NEG_DELAY = 1 << 4
 PU_ERRF_POOL = 1 << 5
 PU_ERRF_PAGES = 1 << 6
+PU_ERRF_PROG = 1 << 7
 
 
 class CacheCfg(C.Structure):

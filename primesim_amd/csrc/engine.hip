@@ -952,8 +952,26 @@ struct Engine {
 
     // ------------------------------------------------------------ sharer sets
     // Line::sharer_set (a std::set<int>, cache.h:86): up to 4 ids inline in
-    // `sh`, ascending, 16 bits each; a fifth sharer moves the set to a full-map
-    // bitmap from the replica's pool (lane k holds word k).
+    // `sh`, ascending, 16 bits each (12 bits each in the stored DirLine word);
+    // a fifth sharer moves the set to a full-map bitmap from the replica's pool
+    // (lane k holds word k).
+    static __device__ __forceinline__ uint64_t dir_word(uint32_t nsh, uint64_t sh, uint32_t st, int prog) {
+        const uint64_t s = nsh == PU_SH_POOL ? sh
+                         : (sh & 0xFFFull) | ((sh >> 4) & 0xFFF000ull) | ((sh >> 8) & 0xFFF000000ull) |
+                           ((sh >> 12) & 0xFFF000000000ull);
+        return s | ((uint64_t)(nsh == PU_SH_POOL ? 7u : nsh) << 48) | ((uint64_t)st << 51) |
+               ((uint64_t)(uint32_t)prog << 54);
+    }
+    static __device__ __forceinline__ uint32_t dir_state(uint64_t w) { return (uint32_t)(w >> 51) & 7u; }
+    static __device__ __forceinline__ int dir_prog(uint64_t w) { return (int)(w >> 54); }
+    static __device__ __forceinline__ void dir_sharers(uint64_t w, uint32_t& nsh, uint64_t& sh) {
+        const uint32_t n = (uint32_t)(w >> 48) & 7u;
+        const uint64_t s = w & 0xFFFFFFFFFFFFull;
+        nsh = n == 7u ? PU_SH_POOL : n;
+        sh = n == 7u ? s
+             : (s & 0xFFFull) | ((s & 0xFFF000ull) << 4) | ((s & 0xFFF000000ull) << 8) |
+               ((s & 0xFFF000000000ull) << 12);
+    }
     __device__ __forceinline__ uint64_t* pool_of(uint64_t idx) const {
         return at<uint64_t>(g->dir.off_pool) + idx * (uint64_t)g->dir.nwords;
     }
@@ -1091,7 +1109,7 @@ struct Engine {
 
     // ------------------------------------------------------------ home slice
     // accessSharedCache (system.cpp:734-893) / accessDirectoryCache (577-731).
-    // The home line is read once (lane w: way w, 32 B) and written once at the
+    // The home line is read once (lane w: way w, 24 B) and written once at the
     // end: nothing reached from here touches directory lines.  Every branch
     // that messages other caches does so first, at timer + access_time, so
     // the branch only chooses the probe; `probe` runs it.
@@ -1117,9 +1135,10 @@ struct Engine {
         if (mine) {
             m = lines[line0 + (uint64_t)ln];
         } else {
-            m.tag = 0; m.id = 0; m.state = ST_I; m.nsh = 0; m._pad = 0; m.sh = 0; m.ts = INT64_MAX;
+            m.tag = 0; m.ts = INT64_MAX; m.w = 0;
         }
-        const uint64_t hm = ballot(mine && m.state != ST_I && m.id == r.prog && m.tag == tag);
+        const uint32_t m_state = dir_state(m.w);
+        const uint64_t hm = ballot(mine && m_state != ST_I && dir_prog(m.w) == r.prog && m.tag == tag);
         int way = hm ? (int)__builtin_ctzll(hm) : -1;
         PROF_ADD(PF_HOME_LD, p_ld);
         count(D.off_cnt, home, 0);
@@ -1136,7 +1155,7 @@ struct Engine {
         bool release_set = false, miss_fill = false;
         if (way < 0 && r.type != PU_WB) {
             // replaceLine (cache.cpp:204-235): first invalid way, else LRU
-            const uint64_t inv = ballot(mine && m.state == ST_I);
+            const uint64_t inv = ballot(mine && m_state == ST_I);
             uint32_t old_st = ST_I;
             uint64_t old_addr = 0;
             int old_prog = 0;
@@ -1144,12 +1163,14 @@ struct Engine {
                 way = (int)__builtin_ctzll(inv);
             } else {
                 way = lru_way(m.ts, mine ? ln : 64, D.nways);
-                old_st = rl32(m.state, way);
-                old_addr = (set << D.offbits) | (rl64(m.tag, way) << (D.offbits + D.idxbits));
-                old_prog = (int)rl32((uint32_t)m.id, way);
             }
-            nsh = rl32(m.nsh, way);
-            sh = rl64(m.sh, way);
+            const uint64_t ww = rl64(m.w, way);
+            if (!inv) {
+                old_st = dir_state(ww);
+                old_addr = (set << D.offbits) | (rl64(m.tag, way) << (D.offbits + D.idxbits));
+                old_prog = dir_prog(ww);
+            }
+            dir_sharers(ww, nsh, sh);
             if (old_st != ST_I) {
                 count(D.off_cnt, home, 2);
                 pr = Req{old_addr, old_prog, PU_RD};
@@ -1173,9 +1194,9 @@ struct Engine {
             *out_state = ST_I;
             return delay;
         } else {
-            st = rl32(m.state, way);
-            nsh = rl32(m.nsh, way);
-            sh = rl64(m.sh, way);
+            const uint64_t ww = rl64(m.w, way);
+            st = dir_state(ww);
+            dir_sharers(ww, nsh, sh);
             if (r.type == PU_WR) {
                 if (st == ST_M || st == ST_E) {
                     pmode = PR_ONE;
@@ -1232,15 +1253,8 @@ struct Engine {
         }
         *out_state = st == ST_B ? ST_S : st;
         if (ln == way) {
-            DirLine nl;
-            nl.tag = tag;
-            nl.id = r.prog;
-            nl.state = (uint8_t)st;
-            nl.nsh = (uint8_t)nsh;
-            nl._pad = 0;
-            nl.sh = sh;
-            nl.ts = timer;                    // home slices stamp the arrival time (Q4)
-            lines[line0 + (uint64_t)way] = nl;
+            // home slices stamp the arrival time (Q4)
+            lines[line0 + (uint64_t)way] = DirLine{tag, timer, dir_word(nsh, sh, st, r.prog)};
         }
         return delay;
     }
@@ -1584,6 +1598,11 @@ struct Engine {
         if (core < 0 || core >= g->num_cores) {
             err_or(PU_ERRF_CORE_RANGE);
             return -1;
+        }
+        if (g->sys_type == 0 && (uint32_t)r_in.prog >= PU_DIR_PROGS) {
+            err_or(PU_ERRF_PROG);             // does not fit the packed directory line
+            stop = true;
+            return 0;
         }
         stat_add(SN_REQS, 1);
         hit = false;

@@ -10,9 +10,9 @@
 //     alive[l] : ncaches x u32 (reference creates caches lazily, system.cpp:172)
 //     cnt[l]   : ncaches x 4 x u64 (ins, miss, evict, wb)
 //   directory / shared-LLC slices (one per network node):
-//     dline    : N*nsets*nways x DirLine (32 B: tag, prog, state, sharers, ts)
+//     dline    : N*nsets*nways x DirLine (24 B: tag, ts, packed prog/state/sharers)
 //                sharers (std::set<int> in the reference, iterated ascending)
-//                are held inline as up to 4 sorted 16-bit ids; a larger set
+//                are held inline as up to 4 sorted 12-bit ids; a larger set
 //                moves to a full-map bitmap taken from a per-replica pool
 //     pool     : pool_entries x nwords x u64 bitmaps + a free stack
 //     dalive, dcnt : per slice
@@ -55,18 +55,23 @@ struct LineMeta {
     uint32_t state;
 };
 
-// Directory / shared-LLC line (reference Line, cache.h:77-87, with sharer_set).
+// Directory / shared-LLC line (reference Line, cache.h:77-87, with sharer_set),
+// 24 B so that more replicas fit in HBM (the directory is ~88% of a replica):
+//   w bits  0-47  sharers: up to 4 LLC ids ascending, 12 bits each (< 4096
+//                 nodes), or the pool index of a full-map bitmap
+//         bits 48-50  sharer count 0..4, 7 = pool
+//         bits 51-53  state
+//         bits 54-63  program id (0..1023; a request with another id stops a
+//                     directory replica with PU_ERRF_PROG)
+// The engine works on the unpacked form (16-bit inline ids, nsh PU_SH_POOL).
 struct DirLine {
     uint64_t tag;
-    int32_t id;
-    uint8_t state;
-    uint8_t nsh;       // 0..4 inline sharers in `sh`; PU_SH_POOL: `sh` is a pool index
-    uint16_t _pad;
-    uint64_t sh;       // inline: ids (16 bits each) ascending from bit 0
     int64_t ts;
+    uint64_t w;
 };
 #define PU_SH_INLINE 4
 #define PU_SH_POOL 0xFF
+#define PU_DIR_PROGS 1024
 
 struct QueueHdr {
     uint32_t head;
