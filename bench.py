@@ -152,13 +152,16 @@ def main() -> None:
     probe = P.UncoreManager()
     probe.init(cfg, replicas=1, device=local)
     rbytes = probe.replica_bytes
+    resident = probe.resident_replicas
     probe.close()
     per_bytes = rbytes + (args.steps + 1) * args.chunk * (REQ_BYTES + 4)
     free, total = torch.cuda.mem_get_info(dev)
-    R = args.replicas or max(1, min(2048, int((free * 0.88) // per_bytes)))
+    # as many replicas as fit in HBM, but no more than the kernel keeps resident
+    # (one wave each): a time-sliced launch over more would run in two rounds
+    R = args.replicas or max(1, min(resident, int((free * 0.88) // per_bytes)))
     R = max(1, R - R % 8) if R >= 8 else R
     log(f"[bench] rank {rank}: replica {rbytes / 2**20:.0f} MiB + requests {(per_bytes - rbytes) / 2**20:.0f} MiB, "
-        f"{R} replicas, free {free / 2**30:.0f} GiB")
+        f"{R} replicas (resident limit {resident}), free {free / 2**30:.0f} GiB")
     global LAST_REPLICAS
     LAST_REPLICAS = R
     um.init(cfg, replicas=R, device=local)

@@ -195,6 +195,10 @@ int        pu_reset(pu_handle* h);
 int        pu_num_replicas(const pu_handle* h);
 /* Device bytes held by one replica's state. */
 uint64_t   pu_replica_bytes(const pu_handle* h);
+/* Replicas this configuration's engine kernel keeps resident on the device at
+ * once (one wave each; registers and LDS bound it).  A launch over more
+ * replicas runs in several rounds.  No reference counterpart (engine sizing). */
+int        pu_resident_replicas(const pu_handle* h);
 
 /* Thread -> core map (reference src/thread_sched.cpp:55-91; identical quirks:
  * first free core, a core is marked busy with prog_id, dealloc frees only

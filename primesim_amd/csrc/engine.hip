@@ -99,7 +99,7 @@ struct QState {
 };
 
 #define AS1 __attribute__((address_space(1)))
-#define PU_RING_PF 8   // staged rings in flight per wave (16 KB LDS)
+#define PU_RING_PF 4   // staged rings in flight per wave (8 KB LDS)
 // native vectors (not classes), so loads/stores through global-address-space
 // pointers need no conversion: slot = {first, second}, header = 10 dwords
 typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
@@ -1129,7 +1129,7 @@ struct Engine {
         if (ln == (home & 63)) at<uint32_t>(D.off_alive)[home] = 1u;   // home_stat[home] = 1
         const uint64_t set = set_index(r.addr, D.offbits, D.nsets);
         const uint64_t tag = r.addr >> (D.offbits + D.idxbits);
-        const uint64_t line0 = ((uint64_t)home * D.nsets + set) * D.nways;
+        const uint64_t line0 = ((uint64_t)home * D.csets + (set >> D.cset_shift)) * D.nways;   // reachable sets only
         const bool mine = (uint64_t)ln < D.nways;
         DirLine m;
         if (mine) {
@@ -1870,6 +1870,23 @@ extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, i
         default: return PU_EINVAL;
     }
     return hipGetLastError() == hipSuccess ? 0 : PU_EIO;
+}
+
+// Replicas (one-wave workgroups) of the time-sliced kernel resident per CU at
+// once: VGPRs and the LDS ring staging bound it.  A launch of more replicas
+// runs the rest only after resident ones finish their slice.
+extern "C" int pu_engine_occupancy(int num_levels, int* blocks_per_cu) {
+    int n = 0;
+    hipError_t e;
+    switch (num_levels) {
+        case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<1, true>, 64, 0); break;
+        case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<2, true>, 64, 0); break;
+        case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<3, true>, 64, 0); break;
+        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<4, true>, 64, 0); break;
+        default: return PU_EINVAL;
+    }
+    *blocks_per_cu = n;
+    return e == hipSuccess ? 0 : PU_EIO;
 }
 
 extern "C" int pu_engine_init_queues(char* arena, uint64_t replica_bytes, uint64_t off_qhdr, uint64_t off_qring,

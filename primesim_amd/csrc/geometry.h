@@ -10,7 +10,9 @@
 //     alive[l] : ncaches x u32 (reference creates caches lazily, system.cpp:172)
 //     cnt[l]   : ncaches x 4 x u64 (ins, miss, evict, wb)
 //   directory / shared-LLC slices (one per network node):
-//     dline    : N*nsets*nways x DirLine (24 B: tag, ts, packed prog/state/sharers)
+//     dline    : N*csets*nways x DirLine (24 B: tag, ts, packed prog/state/sharers);
+//                csets <= nsets: only the sets an address can reach at that
+//                home (DirGeo)
 //                sharers (std::set<int> in the reference, iterated ascending)
 //                are held inline as up to 4 sorted 12-bit ids; a larger set
 //                moves to a full-map bitmap taken from a per-replica pool
@@ -108,10 +110,15 @@ struct LevelGeo {
     uint64_t off_meta, off_ts, off_alive, off_cnt;
 };
 
+// Only the sets some address can reach at a home are stored: the home id and
+// the set index are both taken from the bits above the block offset
+// (system.cpp:921-936, cache.cpp:145-152), so every set a home sees is
+// congruent to it modulo G' = 2^cset_shift.  A home's set s is stored at
+// compact index s >> cset_shift, csets = nsets >> cset_shift per home.
 struct DirGeo {
-    uint64_t nsets, nways, block;
+    uint64_t nsets, nways, block, csets;
     int32_t offbits, idxbits, access_time, nwords;
-    int32_t pool_entries, _pad;
+    int32_t pool_entries, cset_shift;
     uint64_t off_line, off_pool, off_pool_free, off_alive, off_cnt;
 };
 

@@ -39,6 +39,7 @@ extern "C" int pu_engine_unit_network(const Geo* d_geo, char* base, const int32_
                                       hipStream_t s);
 extern "C" int pu_engine_init_queues(char* arena, uint64_t replica_bytes, uint64_t off_qhdr, uint64_t off_qring,
                                      int nqueues, int nreplicas, hipStream_t stream);
+extern "C" int pu_engine_occupancy(int num_levels, int* blocks_per_cu);
 
 namespace pu {
 
@@ -136,6 +137,22 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
     if (y.network.data_width < 1) return pu::set_error(PU_EINVAL, "data_width must be >= 1");
     g->home_offbits = ilog2(dc.block_size);
     g->home_mask_bits = (int)std::ceil(std::log2((double)N));
+    {
+        // Reachable directory sets (DirGeo): with a = addr >> offbits, the raw
+        // home is a mod 2^hb (folded to raw mod 2^(hb-1) when >= N) and the set
+        // is a mod nsets, so a home only sees sets congruent to it modulo
+        // G = gcd(nsets, 2^hb), or 2^(hb-1) when folding can occur.
+        int lg = 0;
+        const int hb = g->home_mask_bits;
+        if (D.offbits == g->home_offbits && hb > 0) {
+            int v2 = 0;
+            while (v2 < 63 && ((D.nsets >> v2) & 1) == 0) v2++;
+            lg = std::min(v2, hb);
+            if ((uint64_t)N < (1ull << hb)) lg = std::min(lg, hb - 1);
+        }
+        D.cset_shift = lg;
+        D.csets = D.nsets >> lg;
+    }
     g->net_type = y.network.net_type;
     g->net_width = g->net_type == 1 ? (int)std::ceil(std::cbrt((double)N)) : (int)std::ceil(std::sqrt((double)N));
     g->header_flits = y.network.header_flits;
@@ -183,12 +200,13 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
     }
     // the bus system has no directory lines (its report still prints the
     // directory block, from counters that stay 0)
-    uint64_t dlines = bus_sys ? 0 : (uint64_t)N * D.nsets * D.nways;
+    uint64_t dlines = bus_sys ? 0 : (uint64_t)N * D.csets * D.nways;
     D.off_line = lay.take(dlines * sizeof(DirLine));
-    // sharer sets of more than 4 LLCs live in pool bitmaps: one entry per 64
-    // directory lines by default (PRIMEUNCORE_POOL_ENTRIES overrides); running
-    // out stops the replica with PU_ERRF_POOL rather than diverge
-    uint64_t pool = bus_sys ? 0 : (dlines / 64 < 64 ? 64 : dlines / 64);
+    // sharer sets of more than 4 LLCs live in pool bitmaps: one entry per
+    // directory line up to 65,536 lines (it cannot run out), one per 64 lines
+    // beyond (PRIMEUNCORE_POOL_ENTRIES overrides); running out stops the
+    // replica with PU_ERRF_POOL rather than diverge
+    uint64_t pool = bus_sys ? 0 : (dlines <= 65536 ? std::max<uint64_t>(dlines, 64) : std::max<uint64_t>(dlines / 64, 65536));
     if (const char* e = std::getenv("PRIMEUNCORE_POOL_ENTRIES"); e && !bus_sys) pool = std::strtoull(e, nullptr, 10);
     if (pool > (1ull << 30)) pool = 1ull << 30;
     D.pool_entries = (int32_t)pool;
@@ -404,6 +422,16 @@ int pu_reset(pu_handle* h) {
 
 int pu_num_replicas(const pu_handle* h) { return h ? h->R : 0; }
 uint64_t pu_replica_bytes(const pu_handle* h) { return h ? h->geo.replica_bytes : 0; }
+
+int pu_resident_replicas(const pu_handle* h) {
+    if (!h) return pu::set_error(PU_EINVAL, "null handle");
+    int per_cu = 0, cus = 0;
+    HIP_TRY(hipSetDevice(h->device), PU_ENODEV);
+    int rc = pu_engine_occupancy(h->geo.num_levels, &per_cu);
+    if (rc) return pu::set_error(rc, "occupancy query failed");
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device), PU_EIO);
+    return per_cu * cus;
+}
 
 int pu_alloc_core(pu_handle* h, int prog_id, int thread_id) {
     if (!h) return pu::set_error(PU_EINVAL, "null handle");

@@ -51,6 +51,7 @@ def lib() -> C.CDLL:
         "pu_reset": (C.c_int, [C.c_void_p]),
         "pu_num_replicas": (C.c_int, [C.c_void_p]),
         "pu_replica_bytes": (C.c_uint64, [C.c_void_p]),
+        "pu_resident_replicas": (C.c_int, [C.c_void_p]),
         "pu_alloc_core": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
         "pu_dealloc_core": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
         "pu_get_core_id": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
@@ -333,6 +334,14 @@ class UncoreManager:
     @property
     def replica_bytes(self) -> int:
         return int(lib().pu_replica_bytes(self._handle()))
+
+    @property
+    def resident_replicas(self) -> int:
+        """Replicas the engine kernel holds resident on the device at once."""
+        n = lib().pu_resident_replicas(self._handle())
+        if n <= 0:
+            raise UncoreError(last_error())
+        return int(n)
 
     def allocCore(self, prog_id: int, thread_id: int) -> int:
         return lib().pu_alloc_core(self._handle(), prog_id, thread_id)
