@@ -206,6 +206,14 @@ int        pu_resident_replicas(const pu_handle* h);
 int pu_alloc_core(pu_handle* h, int prog_id, int thread_id);
 int pu_dealloc_core(pu_handle* h, int prog_id, int thread_id);
 int pu_get_core_id(pu_handle* h, int prog_id, int thread_id);
+/* The same three calls on one replica's own ThreadSched (copied from the
+ * shared one on first use; the shared calls above keep updating it).  The
+ * server (pu_server_*) gives every session (= replica) its own core map, as a
+ * separate prime.cpp process would have.  The replica's report prints its own
+ * core allocation. */
+int pu_alloc_core_replica(pu_handle* h, int replica, int prog_id, int thread_id);
+int pu_dealloc_core_replica(pu_handle* h, int replica, int prog_id, int thread_id);
+int pu_get_core_id_replica(pu_handle* h, int replica, int prog_id, int thread_id);
 
 /* Single-request compatibility path: UncoreManager::uncore_access
  * (uncore_manager.cpp:82-85).  Operates on replica 0; `*addr` is updated in
@@ -221,7 +229,8 @@ int pu_access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n,
                     int32_t* delay_out);
 
 /* Batch path from device memory, all replicas at once, asynchronous on
- * `hip_stream` (a hipStream_t; NULL = the default stream).  Replica r
+ * `hip_stream` (a hipStream_t; NULL = the engine's own stream, see
+ * pu_synchronize).  Replica r
  * processes d_reqs[d_off[r] .. d_off[r+1]) and writes d_delay over the same
  * range.  d_off holds num_replicas+1 entries and lives in device memory.
  * Nothing is copied to or from the host. */
@@ -338,6 +347,86 @@ int        pu_msglog_close(pu_msglog* L);
 int pu_msglog_from_requests(const char* path, const pu_req* reqs, size_t n, const int32_t* thread_prog,
                             const int32_t* thread_id, int num_threads, const int32_t* core_thread,
                             int num_cores);
+
+/* ------------------------------------------------------------------------
+ * Server front-end: prime.cpp's message loop
+ * (reference src/prime.cpp:35-137, main :142-233) behind a Unix-domain socket
+ * instead of MPI, feeding the engine a round at a time.
+ *
+ * A session is one simulation (one prime.cpp process in the reference) and
+ * runs on one replica; its clients are the Pin processes of that simulation,
+ * identified by their rank (the MPI source, = prog_id).  Clients exchange
+ * exactly what core_manager.cpp sends and receives over MPI: MsgMem buffers
+ * (24-B records, common.h:49-59) sent with a tag, and int replies received
+ * on a tag (pu_client_*; INTEGRATION.md shows the core_manager.cpp edit).
+ * Every message is handled with prime.cpp's rules: PROCESS_STARTING /
+ * PROCESS_FINISHING / INTER_PROCESS_BARRIERS maintain the program list and
+ * release barriers (replies on tag 0), NEW_THREAD allocates a core (reply
+ * core % num_recv_threads on tag thread), THREAD_FINISHING frees it,
+ * MEM_REQUESTS runs requests 1..msg[0].addr_dmem-1 with the running delay of
+ * prime.cpp:129 (reply: the batch delay on tag thread), PROGRAM_EXITING ends
+ * one handler thread; a session ends after num_recv_threads of them and
+ * writes its report (UncoreManager::report) to <report_prefix>_<session>.
+ * A negative batch delay stops the session like prime.cpp:130-134 (its
+ * handler exits): the message gets no reply, the report is written, the
+ * session's connections are closed.
+ *
+ * Rounds: each round reads everything the clients have sent, takes from every
+ * session its pending messages up to the first control message that follows
+ * a MEM_REQUESTS message (so control messages never overtake a batch whose
+ * outcome could stop the session), and runs all sessions' MEM_REQUESTS
+ * batches in ONE engine launch (pu_run_device: one wavefront per session),
+ * then sends the replies.  Per session the result is the sequential one of
+ * prime.cpp with one receive thread, in the order the server received the
+ * messages.
+ * ---------------------------------------------------------------------- */
+typedef struct pu_server pu_server;
+
+typedef struct pu_server_opts {
+    const char* socket_path;   /* Unix-domain socket path to listen on */
+    const char* report_prefix; /* session s writes <prefix>_<s> when it ends; NULL = no file */
+    int num_sessions;          /* sessions 0..n-1 (<= replicas); run() returns when all have ended */
+    int num_recv_threads;      /* XmlSim::num_recv_threads (prime.cpp:182); 0 = 1 */
+    int max_msg_size;          /* XmlSim::max_msg_size: records per message beyond the header; 0 = 100 */
+    int verbose;               /* print prime.cpp's "[PriME] ..." progress lines */
+} pu_server_opts;
+
+typedef struct pu_server_stats {
+    uint64_t rounds;           /* service rounds that handled at least one message */
+    uint64_t launches;         /* engine launches (rounds with MEM_REQUESTS) */
+    uint64_t messages;         /* MsgMem messages handled */
+    uint64_t requests;         /* memory requests sent to the engine */
+    int32_t  sessions_ended;
+    int32_t  sessions_halted;  /* stopped by a negative batch delay */
+} pu_server_stats;
+
+/* Host executor: runs one session's requests in order and writes each
+ * request's uncore_access delay (the engine's per-request output).  Lets the
+ * protocol be exercised without a GPU (tests); the product path is
+ * pu_server_create on an engine handle. */
+typedef int (*pu_exec_fn)(void* ctx, int session, const pu_req* reqs, size_t n, int32_t* delays);
+
+/* Serve engine handle h (not owned; sessions <= pu_num_replicas(h)). */
+pu_server* pu_server_create(pu_handle* h, const pu_server_opts* o);
+pu_server* pu_server_create_exec(pu_exec_fn fn, void* ctx, int num_cores, const pu_server_opts* o);
+/* Serve until every session has ended or pu_server_stop; 0 or PU_E*. */
+int  pu_server_run(pu_server* s);
+/* One round, waiting up to timeout_ms for the first message; returns the
+ * number of messages handled (>= 0) or PU_E*. */
+int  pu_server_round(pu_server* s, int timeout_ms);
+void pu_server_stop(pu_server* s);     /* thread-safe */
+int  pu_server_get_stats(pu_server* s, pu_server_stats* out);
+void pu_server_destroy(pu_server* s);
+
+/* Client: the MPI calls of core_manager.cpp.  One client per Pin thread (or a
+ * mutex around a shared one).  send = MPI_Send(records, n*24, MPI_CHAR, 0,
+ * tag); recv = MPI_Recv(value, 1, MPI_INT, 0, tag) with MPI's matching (a
+ * reply sent before the receive is posted waits at the server). */
+typedef struct pu_client pu_client;
+pu_client* pu_client_connect(const char* socket_path, int session, int rank);
+int  pu_client_send(pu_client* c, int tag, const void* records, int n_records);
+int  pu_client_recv(pu_client* c, int tag, int32_t* value);
+void pu_client_close(pu_client* c);
 
 /* ------------------------------------------------------------------------
  * Unit hooks: run one engine component alone on the GPU (one wavefront), for

@@ -104,6 +104,24 @@ class StreamParams(C.Structure):
     ]
 
 
+class ServerOpts(C.Structure):          # pu_server_opts
+    _fields_ = [
+        ("socket_path", C.c_char_p), ("report_prefix", C.c_char_p), ("num_sessions", C.c_int32),
+        ("num_recv_threads", C.c_int32), ("max_msg_size", C.c_int32), ("verbose", C.c_int32),
+    ]
+
+
+class ServerStats(C.Structure):         # pu_server_stats
+    _fields_ = [
+        ("rounds", C.c_uint64), ("launches", C.c_uint64), ("messages", C.c_uint64), ("requests", C.c_uint64),
+        ("sessions_ended", C.c_int32), ("sessions_halted", C.c_int32),
+    ]
+
+
+# pu_exec_fn(ctx, session, reqs, n, delays)
+EXEC_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.c_void_p)
+
+
 # pu_req as a numpy structured dtype (32 bytes, matches the C struct layout)
 REQ_DTYPE = np.dtype([
     ("addr", "<u8"), ("timer", "<i8"), ("core", "<i4"), ("prog_id", "<i4"),

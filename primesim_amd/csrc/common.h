@@ -1,11 +1,42 @@
 // common.h — host-side helpers shared by the C-ABI translation units.
 #pragma once
 
+#include <map>
 #include <string>
+#include <utility>
+#include <vector>
 
 namespace pu {
 
 // Records a message for pu_last_error() and returns `code`.
 int set_error(int code, const std::string& msg);
+
+// ThreadSched (reference src/thread_sched.cpp:55-91) with its quirks: the
+// first free core is taken, a busy core is marked with its prog id, a core is
+// freed only while core_stat == 1, and getCoreId inserts 0 for an unknown
+// (prog, thread) through std::map::operator[].  The map's (prog, thread) order
+// is the order ThreadSched::report prints.
+struct Sched {
+    std::vector<int> stat;
+    std::map<std::pair<int, int>, int> map;
+    int alloc(int prog, int th) {
+        for (size_t i = 0; i < stat.size(); i++)
+            if (stat[i] == 0) {
+                stat[i] = prog;
+                map[{prog, th}] = (int)i;
+                return (int)i;
+            }
+        return -1;
+    }
+    int dealloc(int prog, int th) {
+        int c = map[{prog, th}];
+        if (c >= 0 && c < (int)stat.size() && stat[(size_t)c] == 1) {
+            stat[(size_t)c] = 0;
+            return 1;
+        }
+        return 0;
+    }
+    int get(int prog, int th) { return map[{prog, th}]; }
+};
 
 }  // namespace pu

@@ -51,26 +51,8 @@ constexpr int64_t kProcessStarting = -3, kProcessFinishing = -1, kBarrier = -2, 
 }  // namespace
 
 // ThreadSched for a log replayed without an engine handle (conversion only):
-// the same rules as the handle's (thread_sched.cpp:55-91): first free core,
-// core_stat = prog, free only when core_stat == 1, getCoreId inserts 0.
-struct LocalSched {
-    std::vector<int> stat;
-    std::map<std::pair<int, int>, int> map;
-    int alloc(int prog, int th) {
-        for (size_t i = 0; i < stat.size(); i++)
-            if (stat[i] == 0) {
-                stat[i] = prog;
-                map[{prog, th}] = (int)i;
-                return (int)i;
-            }
-        return -1;
-    }
-    void dealloc(int prog, int th) {
-        int c = map[{prog, th}];
-        if (c >= 0 && c < (int)stat.size() && stat[(size_t)c] == 1) stat[(size_t)c] = 0;
-    }
-    int get(int prog, int th) { return map[{prog, th}]; }
-};
+// the same rules as the handle's (pu::Sched, thread_sched.cpp:55-91).
+using LocalSched = pu::Sched;
 
 struct pu_msglog {
     FILE* f = nullptr;

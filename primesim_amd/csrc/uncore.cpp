@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <sstream>
 #include <string>
@@ -244,9 +245,12 @@ struct pu_handle {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0.0;
-    // ThreadSched (thread_sched.cpp): core_stat + ordered (prog, thread) map
-    std::vector<int> core_stat;
-    std::map<std::pair<int, int>, int> core_map;
+    // ThreadSched (thread_sched.cpp): the shared one, and per-replica copies
+    // made on first use of a per-replica call (pu_*_core_replica: the server's
+    // sessions); the shared calls update both
+    pu::Sched sched;
+    std::vector<std::unique_ptr<pu::Sched>> rsched;
+    pu::Sched& sched_of(int r) { return rsched[(size_t)r] ? *rsched[(size_t)r] : sched; }
     // staging for host-buffer batches
     pu_req* d_reqs = nullptr;
     int32_t* d_delays = nullptr;
@@ -390,7 +394,8 @@ pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device) {
         h->arena = nullptr;
         return fail("hipMalloc of " + std::to_string(bytes) + " bytes for the replica arena failed");
     }
-    h->core_stat.assign((size_t)cfg->sys.num_cores, 0);
+    h->sched.stat.assign((size_t)cfg->sys.num_cores, 0);
+    h->rsched.resize((size_t)num_replicas);
     if (reset_state(h) != 0) {
         std::string m = pu::g_err;
         pu_destroy(h);
@@ -436,31 +441,58 @@ int pu_resident_replicas(const pu_handle* h) {
 int pu_alloc_core(pu_handle* h, int prog_id, int thread_id) {
     if (!h) return pu::set_error(PU_EINVAL, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);
-    for (size_t i = 0; i < h->core_stat.size(); i++) {
-        if (h->core_stat[i] == 0) {
-            h->core_stat[i] = prog_id;
-            h->core_map[{prog_id, thread_id}] = (int)i;
-            return (int)i;
-        }
-    }
-    return -1;
+    for (auto& r : h->rsched)
+        if (r) r->alloc(prog_id, thread_id);
+    return h->sched.alloc(prog_id, thread_id);
 }
 
 int pu_get_core_id(pu_handle* h, int prog_id, int thread_id) {
     if (!h) return pu::set_error(PU_EINVAL, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);
-    return h->core_map[{prog_id, thread_id}];   // operator[]: inserts 0 like the reference
+    for (auto& r : h->rsched)
+        if (r) r->get(prog_id, thread_id);
+    return h->sched.get(prog_id, thread_id);   // operator[]: inserts 0 like the reference
 }
 
 int pu_dealloc_core(pu_handle* h, int prog_id, int thread_id) {
     if (!h) return pu::set_error(PU_EINVAL, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);
-    int core = h->core_map[{prog_id, thread_id}];
-    if (core >= 0 && core < (int)h->core_stat.size() && h->core_stat[(size_t)core] == 1) {
-        h->core_stat[(size_t)core] = 0;
-        return 1;
-    }
-    return 0;
+    for (auto& r : h->rsched)
+        if (r) r->dealloc(prog_id, thread_id);
+    return h->sched.dealloc(prog_id, thread_id);
+}
+
+namespace {
+pu::Sched* replica_sched(pu_handle* h, int replica) {
+    if (replica < 0 || replica >= h->R) return nullptr;
+    auto& r = h->rsched[(size_t)replica];
+    if (!r) r.reset(new pu::Sched(h->sched));
+    return r.get();
+}
+}  // namespace
+
+int pu_alloc_core_replica(pu_handle* h, int replica, int prog_id, int thread_id) {
+    if (!h) return pu::set_error(PU_EINVAL, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    pu::Sched* s = replica_sched(h, replica);
+    if (!s) return pu::set_error(PU_ERANGE, "replica out of range");
+    return s->alloc(prog_id, thread_id);
+}
+
+int pu_dealloc_core_replica(pu_handle* h, int replica, int prog_id, int thread_id) {
+    if (!h) return pu::set_error(PU_EINVAL, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    pu::Sched* s = replica_sched(h, replica);
+    if (!s) return pu::set_error(PU_ERANGE, "replica out of range");
+    return s->dealloc(prog_id, thread_id);
+}
+
+int pu_get_core_id_replica(pu_handle* h, int replica, int prog_id, int thread_id) {
+    if (!h) return pu::set_error(PU_EINVAL, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    pu::Sched* s = replica_sched(h, replica);
+    if (!s) return pu::set_error(PU_ERANGE, "replica out of range");
+    return s->get(prog_id, thread_id);
 }
 
 int pu_access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n, int32_t* delay_out) {
@@ -612,7 +644,7 @@ long pu_report(pu_handle* h, int replica, int include_time, char* buf, size_t ca
     if (include_time) o << "Total computation time: " << h->last_ms / 1000.0 << " seconds\n";
     o << std::endl;
     o << "Core Allocation:\n";
-    for (const auto& kv : h->core_map)
+    for (const auto& kv : h->sched_of(replica).map)
         o << "(proc ID: " << kv.first.first << " ,thread ID: " << kv.first.second << ") => "
           << "core ID: " << kv.second << std::endl;
     o << std::endl;

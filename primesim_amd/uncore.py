@@ -84,6 +84,20 @@ def lib() -> C.CDLL:
         "pu_msglog_from_requests": (C.c_int, [C.c_char_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int,
                                               C.c_void_p, C.c_int]),
         "pu_trace_write": (C.c_int, [C.c_char_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int]),
+        "pu_alloc_core_replica": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
+        "pu_dealloc_core_replica": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
+        "pu_get_core_id_replica": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
+        "pu_server_create": (C.c_void_p, [C.c_void_p, P(A.ServerOpts)]),
+        "pu_server_create_exec": (C.c_void_p, [A.EXEC_FN, C.c_void_p, C.c_int, P(A.ServerOpts)]),
+        "pu_server_run": (C.c_int, [C.c_void_p]),
+        "pu_server_round": (C.c_int, [C.c_void_p, C.c_int]),
+        "pu_server_stop": (None, [C.c_void_p]),
+        "pu_server_get_stats": (C.c_int, [C.c_void_p, P(A.ServerStats)]),
+        "pu_server_destroy": (None, [C.c_void_p]),
+        "pu_client_connect": (C.c_void_p, [C.c_char_p, C.c_int, C.c_int]),
+        "pu_client_send": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int]),
+        "pu_client_recv": (C.c_int, [C.c_void_p, C.c_int, P(C.c_int32)]),
+        "pu_client_close": (None, [C.c_void_p]),
         "pu_unit_queue_run": (C.c_int, [C.c_uint64, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
                                         P(C.c_uint64), C.c_int]),
         "pu_unit_network_run": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64,
