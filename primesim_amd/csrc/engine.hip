@@ -237,6 +237,22 @@ __device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, RM, 0xF, false);
     return ((uint64_t)hi << 32) | lo;
 }
+// The same scan on 32 bits: one v_add_u32 with a DPP source per step
+// (bound_ctrl: lanes without a source add 0).  Exact when the 64 terms sum
+// below 2^32 (the caller checks every term < 2^26).
+template <int CTRL, int RM>
+__device__ __forceinline__ uint32_t dpp_u32z(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xF, true);
+}
+__device__ __forceinline__ uint32_t scan_incl_u32(uint32_t v) {
+    v += dpp_u32z<0x111, 0xF>(v);
+    v += dpp_u32z<0x112, 0xF>(v);
+    v += dpp_u32z<0x114, 0xF>(v);
+    v += dpp_u32z<0x118, 0xF>(v);
+    v += dpp_u32z<0x142, 0xA>(v);
+    v += dpp_u32z<0x143, 0xC>(v);
+    return v;
+}
 __device__ __forceinline__ uint64_t scan_incl_u64(uint64_t v) {
     v += dpp_u64<0x111, 0xF>(v);   // row_shr:1
     v += dpp_u64<0x112, 0xF>(v);   // row_shr:2
@@ -700,7 +716,10 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         while (js < nh) {
             const bool live = ln >= js && ln < nh;
             const uint64_t e = live ? vd + c.link_delay + c.router : 0;
-            const uint64_t S = scan_incl_u64(e);
+            // per-hop terms are small except past a saturated queue: a 32-bit
+            // scan then gives the same sums with a quarter of the VALU work
+            const uint64_t S = ballot(e >= (1ull << 26)) == 0 ? (uint64_t)scan_incl_u32((uint32_t)e)
+                                                                : scan_incl_u64(e);
             const uint64_t A = t + c.router + (S - e);       // arrival of hop ln (after its router)
             const uint64_t cand = ballot(live && vfront <= A + (uint64_t)plen);
             const int jt = cand ? (int)__builtin_ctzll(cand) : nh;
