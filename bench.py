@@ -249,7 +249,7 @@ def main() -> None:
     pos = d_pos.cpu().numpy().view(np.uint64)
     adv = (pos - win_off[:-1]).astype(np.int64)
     log(f"[bench] requests per replica in the timed window: min {adv.min()} median {int(np.median(adv))} "
-        f"max {adv.max()} of {W_t}")
+        f"max {adv.max()} of {W_t}; {int((adv >= W_t).sum())} at the end (halted replicas skip to it)")
     rep0.append(d_win_delay[:int(adv[0])].cpu().numpy())
     gen.close()
 
