@@ -125,7 +125,8 @@ typedef struct pu_req {
     int32_t  prog_id;      /* program (Pin process rank, >= 1) */
     uint8_t  mem_type;     /* PU_RD / PU_WR */
     uint8_t  batch_start;  /* 1 = first request of a message */
-    uint16_t _pad0;
+    uint16_t tag;          /* MPI tag of its message = receive-thread id (prime.cpp:53);
+                              only the server's per-thread stop reads it, 0 elsewhere */
     int32_t  _pad1;
 } pu_req;                  /* 32 bytes */
 
@@ -171,13 +172,20 @@ typedef struct pu_stats {
 #define PU_ERRF_EMPTY_SHARER (1ull << 2)  /* *sharer_set.begin() on empty set */
 #define PU_ERRF_QUEUE        (1ull << 3)  /* queue-model precondition violated */
 #define PU_ERRF_NEG_DELAY    (1ull << 4)  /* batch delay went negative (prime.cpp:130) */
-#define PU_ERRF_POOL         (1ull << 5)  /* sharer-bitmap pool exhausted (engine limit;
-                                             raise PRIMEUNCORE_POOL_ENTRIES) */
-#define PU_ERRF_PAGES        (1ull << 6)  /* page table 3/4 full (engine limit;
+#define PU_ERRF_POOL         (1ull << 5)  /* sharer-bitmap pool exhausted (engine limit: the
+                                             pool holds one entry per directory line up to
+                                             2 GiB of bitmaps; PRIMEUNCORE_POOL_ENTRIES) */
+#define PU_ERRF_PAGES        (1ull << 6)  /* page table 3/4 full (engine limit: 2^22 slots,
                                              raise PRIMEUNCORE_PAGE_ENTRIES) */
-#define PU_ERRF_PROG         (1ull << 7)  /* prog_id outside [0, 1024) in a directory
-                                             system (engine limit: packed directory
-                                             lines; the replica stops at that request) */
+#define PU_ERRF_PROG         (1ull << 7)  /* no longer raised (directory lines hold the
+                                             full int prog_id since 0.2) */
+/* The bits that mean the replica stopped where the reference would have
+ * continued (an engine limit) or reached a state the reference leaves undefined.
+ * Not CORE_RANGE (System::access returns -1 and goes on) nor NEG_DELAY
+ * (prime.cpp's own stop).  The host batch paths and the server return /
+ * report PU_ESTATE for these. */
+#define PU_ERRF_LIMITS (PU_ERRF_WB_MISS | PU_ERRF_EMPTY_SHARER | PU_ERRF_QUEUE | \
+                        PU_ERRF_POOL | PU_ERRF_PAGES | PU_ERRF_PROG)
 
 /* ------------------------------------------------------------------------
  * Engine lifetime and the hot path.
@@ -215,16 +223,33 @@ int pu_alloc_core_replica(pu_handle* h, int replica, int prog_id, int thread_id)
 int pu_dealloc_core_replica(pu_handle* h, int replica, int prog_id, int thread_id);
 int pu_get_core_id_replica(pu_handle* h, int replica, int prog_id, int thread_id);
 
+/* Replay of the recorded timers (no reference counterpart; the rule is the
+ * core side's, core_manager.cpp:265 `cycle += delay` after every reply):
+ *   PU_REPLAY_OPEN   (default) timer_i is used as recorded;
+ *   PU_REPLAY_CLOSED timer_i += the sum of the batch delays of that core's
+ *                    earlier messages, as if the recording core had waited for
+ *                    each reply.  The uncore (System) is untouched. */
+#define PU_REPLAY_OPEN   0
+#define PU_REPLAY_CLOSED 1
+int pu_set_replay_mode(pu_handle* h, int mode);
+
+/* PU_ERRF_* bits of replicas [0, n) (EngineStats.error_flags). */
+int pu_error_flags(pu_handle* h, uint64_t* out, size_t n);
+
 /* Single-request compatibility path: UncoreManager::uncore_access
  * (uncore_manager.cpp:82-85).  Operates on replica 0; `*addr` is updated in
- * place like InsMem::addr_dmem (system.cpp:916).  Returns the delay (>= 0)
- * or -1 for core_id >= num_cores, like System::access (system.cpp:147-150). */
+ * place like InsMem::addr_dmem (system.cpp:916).  Returns the delay (an int,
+ * negative when the reference's int wraps) or -1 for core_id >= num_cores,
+ * like System::access (system.cpp:147-150).  No prime.cpp halt rule and no
+ * closed-loop shift apply here: those belong to the caller's message loop. */
 int pu_access(pu_handle* h, int core_id, int prog_id, int mem_type,
               uint64_t* addr, int64_t timer);
 
 /* Batch path from host memory: the per-message loop of prime.cpp:120-137 for
  * replica `replica`.  delay_out[i] receives uncore_access's return value for
- * reqs[i] (may be NULL).  Synchronous.  Returns 0 or PU_E*. */
+ * reqs[i] (may be NULL).  Synchronous.  Returns 0 or PU_E*; PU_ESTATE when
+ * the replica carries a PU_ERRF_LIMITS bit (an engine limit stopped it where
+ * the reference would continue: later delays are 0, not the reference's). */
 int pu_access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n,
                     int32_t* delay_out);
 
@@ -367,9 +392,12 @@ int pu_msglog_from_requests(const char* path, const pu_req* reqs, size_t n, cons
  * prime.cpp:129 (reply: the batch delay on tag thread), PROGRAM_EXITING ends
  * one handler thread; a session ends after num_recv_threads of them and
  * writes its report (UncoreManager::report) to <report_prefix>_<session>.
- * A negative batch delay stops the session like prime.cpp:130-134 (its
- * handler exits): the message gets no reply, the report is written, the
- * session's connections are closed.
+ * A negative batch delay stops that message's receive thread like
+ * prime.cpp:130-134 (its handler returns): the message gets no reply, later
+ * messages on its tag are never received, and once every receive thread has
+ * returned the report is written and the session's connections are closed.
+ * An engine limit (PU_ERRF_LIMITS) ends the session with an error instead of
+ * replying with delays that are no longer the reference's.
  *
  * Rounds: each round reads everything the clients have sent, takes from every
  * session its pending messages up to the first control message that follows
@@ -397,13 +425,16 @@ typedef struct pu_server_stats {
     uint64_t messages;         /* MsgMem messages handled */
     uint64_t requests;         /* memory requests sent to the engine */
     int32_t  sessions_ended;
-    int32_t  sessions_halted;  /* stopped by a negative batch delay */
+    int32_t  sessions_halted;  /* a receive thread stopped by a negative batch delay */
+    int32_t  sessions_failed;  /* ended by an engine limit (PU_ERRF_LIMITS): no exact reply possible */
+    int32_t  _pad;
 } pu_server_stats;
 
 /* Host executor: runs one session's requests in order and writes each
  * request's uncore_access delay (the engine's per-request output).  Lets the
  * protocol be exercised without a GPU (tests); the product path is
- * pu_server_create on an engine handle. */
+ * pu_server_create on an engine handle.  Returns 0, a negative PU_E* (the
+ * round fails), or positive PU_ERRF_* bits the session's replica now carries. */
 typedef int (*pu_exec_fn)(void* ctx, int session, const pu_req* reqs, size_t n, int32_t* delays);
 
 /* Serve engine handle h (not owned; sessions <= pu_num_replicas(h)). */

@@ -42,6 +42,7 @@ def oracle_lib() -> C.CDLL:
         L.cpuref_run.restype = C.c_long
         L.cpuref_run.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
         L.cpuref_stats.argtypes = [C.c_void_p, P(A.Stats)]
+        L.cpuref_set_mode.argtypes = [C.c_void_p, C.c_int]
         L.cpuref_completion.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.cpuref_cache_counters.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]
         L.cpuref_queue_run.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
@@ -72,6 +73,7 @@ def ref_lib() -> C.CDLL:
         L.ref_run.restype = C.c_long
         L.ref_run.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
         L.ref_completion.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.ref_set_mode.argtypes = [C.c_void_p, C.c_int]
         L.ref_report.restype = C.c_long
         L.ref_report.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t]
         L.ref_counters.argtypes = [C.c_void_p]
@@ -113,6 +115,10 @@ class CpuRef:
         rc = oracle_lib().cpuref_run(self._h, reqs.ctypes.data, len(reqs), d.ctypes.data)
         return d, int(rc)
 
+    def set_mode(self, mode: int) -> None:
+        """MODE_CLOSED (closed-loop replay) | MODE_NOHALT (System::access semantics)."""
+        oracle_lib().cpuref_set_mode(self._h, mode)
+
     def stats(self) -> A.Stats:
         s = A.Stats()
         oracle_lib().cpuref_stats(self._h, C.byref(s))
@@ -150,6 +156,9 @@ def cpuref_network(nodes: int, net_type: int, data_width: int, header_flits: int
                                     inject_delay, src.ctypes.data, dst.ctypes.data, ln.ctypes.data,
                                     timer.ctypes.data, len(src), out.ctypes.data, C.byref(st))
     return out, st
+
+
+MODE_CLOSED, MODE_NOHALT, MODE_MSGHALT = 1, 2, 4   # oracle/cpu_ref.h CPUREF_*
 
 
 REF_COUNTER_NAMES = ("link_visits", "link_flits", "mg1_calls", "lockdown_calls", "bus_accesses",
@@ -190,6 +199,9 @@ class RefUncore:
         out = np.zeros(self.num_cores, dtype=np.int64)
         ref_lib().ref_completion(self._h, out.ctypes.data, self.num_cores)
         return out
+
+    def set_mode(self, mode: int) -> None:
+        ref_lib().ref_set_mode(self._h, mode)
 
     def report(self) -> str:
         fd, tmp = tempfile.mkstemp(suffix=".report")

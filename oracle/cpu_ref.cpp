@@ -216,6 +216,10 @@ struct Sys {
     std::vector<int64_t> completion;
     int batch_delay = 0;   // running delay of the open message, kept across cpuref_run calls
     bool halted = false;   // prime.cpp:130-134: the handler exits on a negative delay
+    int mode = 0;          // CPUREF_CLOSED | CPUREF_NOHALT
+    std::vector<int64_t> core_shift;   // closed loop: the core's summed batch delays
+    int64_t msg_shift = 0;             // closed loop: the open message's shift
+    bool skip_msg = false;             // CPUREF_MSGHALT: the open message went negative
 
     // -------------------------------------------------- geometry
     std::string init(const pu_sim_cfg* c) {
@@ -292,6 +296,7 @@ struct Sys {
         st.num_levels = L;
         core_stat.assign((size_t)cores, 0);
         completion.assign((size_t)cores, -1);
+        core_shift.assign((size_t)cores, 0);
         return "";
     }
 
@@ -848,20 +853,39 @@ int cpuref_alloc_core(void* h, int prog, int thread) {
 
 long cpuref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
     Sys* s = (Sys*)h;
-    if (s->halted) {
+    const bool closed = (s->mode & CPUREF_CLOSED) != 0, keep_halt = (s->mode & CPUREF_NOHALT) == 0;
+    if (s->halted && keep_halt) {
         if (delays) std::fill_n(delays, n, 0);
         return n ? -1 : 0;
     }
+    const bool msghalt = (s->mode & 4) != 0;
     int delay = s->batch_delay;
     for (size_t i = 0; i < n; i++) {
         const pu_req& q = reqs[i];
-        if (q.batch_start) delay = 0;
-        int64_t t = q.timer + delay;
+        const bool core_ok = q.core >= 0 && q.core < s->cores;
+        if (q.batch_start) {
+            delay = 0;
+            s->skip_msg = false;
+            if (closed && core_ok) s->msg_shift = s->core_shift[(size_t)q.core];
+        }
+        if (s->skip_msg) {          // MSGHALT: this message's handler thread has returned
+            if (delays) delays[i] = 0;
+            continue;
+        }
+        int64_t t = q.timer + (closed ? s->msg_shift : 0) + delay;
         int d = s->access(q.core, Req{q.addr, q.prog_id, (int)q.mem_type}, t);
         if (delays) delays[i] = d;
         delay += d - 1;
-        if (q.core >= 0 && q.core < s->cores) s->completion[(size_t)q.core] = t + d;
-        if (delay < 0) {
+        if (core_ok) {
+            s->completion[(size_t)q.core] = t + d;
+            if (closed) s->core_shift[(size_t)q.core] = s->msg_shift + delay;
+        }
+        if (delay < 0 && msghalt) {
+            s->st.error_flags |= PU_ERRF_NEG_DELAY;
+            s->skip_msg = true;
+            continue;
+        }
+        if (delay < 0 && keep_halt) {
             s->st.error_flags |= PU_ERRF_NEG_DELAY;
             s->batch_delay = delay;
             s->halted = true;
@@ -870,6 +894,11 @@ long cpuref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
         }
     }
     s->batch_delay = delay;
+    return 0;
+}
+
+int cpuref_set_mode(void* h, int mode) {
+    ((Sys*)h)->mode = mode;
     return 0;
 }
 

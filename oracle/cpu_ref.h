@@ -20,6 +20,13 @@ int cpuref_alloc_core(void* h, int prog, int thread);
 /* prime.cpp:120-137 loop over reqs; delays may be NULL.  Returns 0 or the
  * index+1 of the first request whose running batch delay went negative. */
 long cpuref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays);
+/* Replay mode bits: closed loop (timer_i += the core's earlier batch delays,
+ * core_manager.cpp:265), no halt (System::access semantics), and the per-
+ * message stop of one receive thread among several (the server). */
+#define CPUREF_CLOSED 1
+#define CPUREF_NOHALT 2
+#define CPUREF_MSGHALT 4   /* a negative running delay skips the rest of that message only */
+int cpuref_set_mode(void* h, int mode);
 int cpuref_stats(void* h, pu_stats* out);
 int cpuref_completion(void* h, int64_t* out, size_t n);
 /* Per-cache counters: level l (0..num_levels-1) or l == num_levels for the

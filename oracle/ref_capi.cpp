@@ -80,6 +80,10 @@ struct RefInstance {
     int batch_delay = 0;   // prime.cpp's running `delay` of the open message, kept across calls
     bool halted = false;   // prime.cpp:130-134: the handler thread exits on a negative delay
     std::vector<int64_t> completion;
+    int mode = 0;                      // 1 closed loop, 2 no halt (as oracle/cpu_ref.h)
+    std::vector<int64_t> core_shift;   // closed loop: the core's summed batch delays (core_manager.cpp:265)
+    int64_t msg_shift = 0;
+    bool skip_msg = false;             // mode 4: the open message went negative, its rest is skipped
 };
 
 static std::string slurp(const char* path) {
@@ -103,6 +107,7 @@ void* ref_create(const char* xml_path, int* err) {
     r->sched.init(r->sys.getCoreCount());
     r->num_cores = r->sys.getCoreCount();
     r->completion.assign((size_t)r->num_cores, -1);
+    r->core_shift.assign((size_t)r->num_cores, 0);
     reset_counters();
     if (err) *err = 0;
     return r;
@@ -153,25 +158,43 @@ int ref_get_core_id(void* h, int prog, int thread) {
 // negative (prime.cpp:130 would kill the handler thread there).
 long ref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
     RefInstance* r = (RefInstance*)h;
-    if (r->halted) {
+    const bool closed = (r->mode & 1) != 0, keep_halt = (r->mode & 2) == 0;
+    if (r->halted && keep_halt) {
         if (delays) std::fill_n(delays, n, 0);
         return n ? -1 : 0;
     }
+    const bool msghalt = (r->mode & 4) != 0;
     int delay = r->batch_delay;   // prime.cpp:113 `delay` is an int
     InsMem ins;
     std::memset(&ins, 0, sizeof(ins));
     for (size_t i = 0; i < n; i++) {
         const pu_req& q = reqs[i];
-        if (q.batch_start) delay = 0;
+        const bool core_ok = q.core >= 0 && q.core < r->num_cores;
+        if (q.batch_start) {
+            delay = 0;
+            r->skip_msg = false;
+            if (closed && core_ok) r->msg_shift = r->core_shift[(size_t)q.core];
+        }
+        if (r->skip_msg) {          // MSGHALT: this message's handler thread has returned
+            if (delays) delays[i] = 0;
+            continue;
+        }
         ins.prog_id = q.prog_id;
         ins.mem_type = (char)q.mem_type;
         ins.addr_dmem = q.addr;
-        int64_t t = q.timer + delay;
+        int64_t t = q.timer + (closed ? r->msg_shift : 0) + delay;
         int d = r->sys.access(q.core, &ins, t);
         if (delays) delays[i] = d;
         delay += d - 1;
-        if (q.core >= 0 && q.core < r->num_cores) r->completion[(size_t)q.core] = t + d;
-        if (delay < 0) {
+        if (core_ok) {
+            r->completion[(size_t)q.core] = t + d;
+            if (closed) r->core_shift[(size_t)q.core] = r->msg_shift + delay;
+        }
+        if (delay < 0 && msghalt) {
+            r->skip_msg = true;
+            continue;
+        }
+        if (delay < 0 && keep_halt) {
             r->batch_delay = delay;
             r->halted = true;
             if (delays) std::fill(delays + i + 1, delays + n, 0);
@@ -179,6 +202,11 @@ long ref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
         }
     }
     r->batch_delay = delay;
+    return 0;
+}
+
+int ref_set_mode(void* h, int mode) {
+    ((RefInstance*)h)->mode = mode;
     return 0;
 }
 

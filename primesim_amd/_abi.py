@@ -27,6 +27,7 @@ PU_ERRF_NEG_DELAY = 1 << 4
 PU_ERRF_POOL = 1 << 5
 PU_ERRF_PAGES = 1 << 6
 PU_ERRF_PROG = 1 << 7
+PU_ERRF_LIMITS = PU_ERRF_WB_MISS | PU_ERRF_EMPTY_SHARER | PU_ERRF_QUEUE | PU_ERRF_POOL | PU_ERRF_PAGES | PU_ERRF_PROG
 
 
 class CacheCfg(C.Structure):
@@ -115,6 +116,7 @@ class ServerStats(C.Structure):         # pu_server_stats
     _fields_ = [
         ("rounds", C.c_uint64), ("launches", C.c_uint64), ("messages", C.c_uint64), ("requests", C.c_uint64),
         ("sessions_ended", C.c_int32), ("sessions_halted", C.c_int32),
+        ("sessions_failed", C.c_int32), ("_pad", C.c_int32),
     ]
 
 
@@ -125,7 +127,7 @@ EXEC_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.c_
 # pu_req as a numpy structured dtype (32 bytes, matches the C struct layout)
 REQ_DTYPE = np.dtype([
     ("addr", "<u8"), ("timer", "<i8"), ("core", "<i4"), ("prog_id", "<i4"),
-    ("mem_type", "u1"), ("batch_start", "u1"), ("_pad0", "<u2"), ("_pad1", "<i4"),
+    ("mem_type", "u1"), ("batch_start", "u1"), ("tag", "<u2"), ("_pad1", "<i4"),
 ])
 assert REQ_DTYPE.itemsize == 32
 assert C.sizeof(SimCfg) == 24 + C.sizeof(SysCfg)

@@ -6,10 +6,17 @@
 #include <utility>
 #include <vector>
 
+#include "../../include/primeuncore.h"
+
 namespace pu {
 
 // Records a message for pu_last_error() and returns `code`.
 int set_error(int code, const std::string& msg);
+
+// pu_run_device with extra kernel flags (PU_KF_*, geometry.h): the server's
+// per-receive-thread stop.
+int run_device_flags(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
+                     uint32_t extra_flags);
 
 // ThreadSched (reference src/thread_sched.cpp:55-91) with its quirks: the
 // first free core is taken, a busy core is marked with its prog id, a core is

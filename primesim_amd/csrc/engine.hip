@@ -981,15 +981,13 @@ struct Engine {
     // `sh`, ascending, 16 bits each (12 bits each in the stored DirLine word);
     // a fifth sharer moves the set to a full-map bitmap from the replica's pool
     // (lane k holds word k).
-    static __device__ __forceinline__ uint64_t dir_word(uint32_t nsh, uint64_t sh, uint32_t st, int prog) {
+    static __device__ __forceinline__ uint64_t dir_word(uint32_t nsh, uint64_t sh, uint32_t st) {
         const uint64_t s = nsh == PU_SH_POOL ? sh
                          : (sh & 0xFFFull) | ((sh >> 4) & 0xFFF000ull) | ((sh >> 8) & 0xFFF000000ull) |
                            ((sh >> 12) & 0xFFF000000000ull);
-        return s | ((uint64_t)(nsh == PU_SH_POOL ? 7u : nsh) << 48) | ((uint64_t)st << 51) |
-               ((uint64_t)(uint32_t)prog << 54);
+        return s | ((uint64_t)(nsh == PU_SH_POOL ? 7u : nsh) << 48) | ((uint64_t)st << 51);
     }
     static __device__ __forceinline__ uint32_t dir_state(uint64_t w) { return (uint32_t)(w >> 51) & 7u; }
-    static __device__ __forceinline__ int dir_prog(uint64_t w) { return (int)(w >> 54); }
     static __device__ __forceinline__ void dir_sharers(uint64_t w, uint32_t& nsh, uint64_t& sh) {
         const uint32_t n = (uint32_t)(w >> 48) & 7u;
         const uint64_t s = w & 0xFFFFFFFFFFFFull;
@@ -1161,10 +1159,10 @@ struct Engine {
         if (mine) {
             m = lines[line0 + (uint64_t)ln];
         } else {
-            m.tag = 0; m.ts = INT64_MAX; m.w = 0;
+            m.tag = 0; m.ts = INT64_MAX; m.w = 0; m.prog = 0; m._pad = 0;
         }
         const uint32_t m_state = dir_state(m.w);
-        const uint64_t hm = ballot(mine && m_state != ST_I && dir_prog(m.w) == r.prog && m.tag == tag);
+        const uint64_t hm = ballot(mine && m_state != ST_I && m.prog == r.prog && m.tag == tag);
         int way = hm ? (int)__builtin_ctzll(hm) : -1;
         PROF_ADD(PF_HOME_LD, p_ld);
         count(D.off_cnt, home, 0);
@@ -1194,7 +1192,7 @@ struct Engine {
             if (!inv) {
                 old_st = dir_state(ww);
                 old_addr = (set << D.offbits) | (rl64(m.tag, way) << (D.offbits + D.idxbits));
-                old_prog = dir_prog(ww);
+                old_prog = (int)rl32((uint32_t)m.prog, way);
             }
             dir_sharers(ww, nsh, sh);
             if (old_st != ST_I) {
@@ -1280,7 +1278,7 @@ struct Engine {
         *out_state = st == ST_B ? ST_S : st;
         if (ln == way) {
             // home slices stamp the arrival time (Q4)
-            lines[line0 + (uint64_t)way] = DirLine{tag, timer, dir_word(nsh, sh, st, r.prog)};
+            lines[line0 + (uint64_t)way] = DirLine{tag, timer, dir_word(nsh, sh, st), r.prog, 0u};
         }
         return delay;
     }
@@ -1625,11 +1623,6 @@ struct Engine {
             err_or(PU_ERRF_CORE_RANGE);
             return -1;
         }
-        if (g->sys_type == 0 && (uint32_t)r_in.prog >= PU_DIR_PROGS) {
-            err_or(PU_ERRF_PROG);             // does not fit the packed directory line
-            stop = true;
-            return 0;
-        }
         stat_add(SN_REQS, 1);
         hit = false;
         dly = 0;
@@ -1693,7 +1686,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PU_MIN_WAVES
                                                     int replica0, const pu_req* __restrict__ reqs,
                                                     const uint64_t* __restrict__ off,
                                                     int32_t* __restrict__ delays, uint64_t* __restrict__ pos,
-                                                    uint64_t budget_ticks) {
+                                                    uint64_t budget_ticks, uint32_t flags) {
     if constexpr (!SLICED) {
         pos = nullptr;
         budget_ticks = 0;
@@ -1712,7 +1705,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PU_MIN_WAVES
 
     RunState* rs = e.template at<RunState>(g->off_run);
     int32_t D = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->batch_delay : 0u, 0);
-    int32_t halted = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->halted : 0u, 0);
+    const int32_t halted0 = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->halted : 0u, 0);
+    const bool keep_halt = (flags & PU_KF_NOHALT) == 0;
+    int32_t halted = keep_halt ? halted0 : 0;
+    int32_t skip_msg = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->skip_msg : 0u, 0);
+    int64_t msg_shift = (int64_t)rl64(e.ln == 0 ? (uint64_t)rs->msg_shift : 0ull, 0);
+    uint64_t dead_tags = rl64(e.ln == 0 ? rs->dead_tags : 0ull, 0);
+    int64_t* core_shift = e.template at<int64_t>(g->off_core_shift);
     e.pool_top = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->pool_top : 0u, 0);
     e.page_next = rl64(e.ln == 0 ? rs->page_next : 0ull, 0);
     e.last_addr = rl64(e.ln == 0 ? rs->last_addr : 0ull, 0);
@@ -1729,28 +1728,52 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PU_MIN_WAVES
         }
         PROF_T(p_loop);
         const pu_req q = reqs[i];
-        if (q.batch_start) D = 0;
+        const bool core_ok = q.core >= 0 && q.core < g->num_cores;
+        if (q.batch_start) {
+            D = 0;
+            skip_msg = (flags & PU_KF_MSGHALT) ? (int32_t)((dead_tags >> (q.tag & 63)) & 1) : 0;
+            if ((flags & PU_KF_CLOSED) && core_ok)
+                msg_shift = (int64_t)rl64(e.ln == 0 ? (uint64_t)core_shift[q.core] : 0ull, 0);
+        }
+        if (skip_msg) {                     // PU_KF_MSGHALT: this message's handler thread has exited
+            if (e.ln == 0) delays[i] = 0;
+            continue;
+        }
         PROF_ADD(PF_REQ, p_loop);
-        const int64_t t = q.timer + D;
+        const int64_t t = q.timer + ((flags & PU_KF_CLOSED) ? msg_shift : 0) + D;
         Req r{q.addr, q.prog_id, (int32_t)q.mem_type};
         int d = e.access(q.core, r, t);
+        D += d - 1;
         if (e.ln == 0) {
             delays[i] = d;
-            if (q.core >= 0 && q.core < g->num_cores) completion[q.core] = t + d;
+            if (core_ok) {
+                completion[q.core] = t + d;
+                if (flags & PU_KF_CLOSED) core_shift[q.core] = msg_shift + D;
+            }
         }
         done++;
-        D += d - 1;
         if (D < 0) {                        // prime.cpp:130-134
             err_or(PU_ERRF_NEG_DELAY);
-            halted = 1;
+            if (flags & PU_KF_MSGHALT) {
+                skip_msg = 1;
+                dead_tags |= 1ull << (q.tag & 63);
+            } else if (keep_halt) {
+                halted = 1;
+            }
         }
-        if (e.stop) halted = 1;            // engine limit hit (sharer pool): cannot continue exactly
+        if (e.stop) {                       // engine limit hit: cannot continue exactly
+            halted = 1;
+            skip_msg = 0;
+        }
         PROF_ADD(PF_LOOP, p_loop);
     }
     if (e.ln == 0) {
         if (pos) pos[blockIdx.x] = i;
         rs->batch_delay = D;
-        rs->halted = halted;
+        rs->halted = keep_halt ? halted : (halted0 | halted);
+        rs->skip_msg = skip_msg;
+        rs->msg_shift = msg_shift;
+        rs->dead_tags = dead_tags;
         rs->processed += done;
         rs->pool_top = e.pool_top;
         rs->page_next = e.page_next;
@@ -1880,13 +1903,13 @@ extern "C" int pu_engine_unit_network(const Geo* d_geo, char* base, const int32_
 // ---------------------------------------------------------------- launchers
 extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,
                                 const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
-                                uint64_t budget_ticks, hipStream_t stream) {
+                                uint64_t budget_ticks, uint32_t flags, hipStream_t stream) {
     dim3 grid((unsigned)nblocks), block(64);
 #define PU_LAUNCH(L)                                                                                              \
     if (pos) hipLaunchKernelGGL((uncore_kernel<L, true>), grid, block, 0, stream, d_geo, arena, replica0, reqs, off, \
-                                delays, pos, budget_ticks);                                                      \
+                                delays, pos, budget_ticks, flags);                                               \
     else hipLaunchKernelGGL((uncore_kernel<L, false>), grid, block, 0, stream, d_geo, arena, replica0, reqs, off,   \
-                            delays, pos, budget_ticks);
+                            delays, pos, budget_ticks, flags);
     switch (num_levels) {
         case 1: PU_LAUNCH(1); break;
         case 2: PU_LAUNCH(2); break;

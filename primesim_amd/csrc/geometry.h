@@ -58,22 +58,22 @@ struct LineMeta {
 };
 
 // Directory / shared-LLC line (reference Line, cache.h:77-87, with sharer_set),
-// 24 B so that more replicas fit in HBM (the directory is ~88% of a replica):
+// 32 B (two 16-B loads per way):
 //   w bits  0-47  sharers: up to 4 LLC ids ascending, 12 bits each (< 4096
 //                 nodes), or the pool index of a full-map bitmap
 //         bits 48-50  sharer count 0..4, 7 = pool
 //         bits 51-53  state
-//         bits 54-63  program id (0..1023; a request with another id stops a
-//                     directory replica with PU_ERRF_PROG)
+//   prog  the program id (InsMem::prog_id, any int)
 // The engine works on the unpacked form (16-bit inline ids, nsh PU_SH_POOL).
 struct DirLine {
     uint64_t tag;
     int64_t ts;
     uint64_t w;
+    int32_t prog;
+    uint32_t _pad;
 };
 #define PU_SH_INLINE 4
 #define PU_SH_POOL 0xFF
-#define PU_DIR_PROGS 1024
 
 struct QueueHdr {
     uint32_t head;
@@ -154,8 +154,18 @@ struct Geo {
     DirGeo dir;
     TlbGeo tlb;
     uint64_t off_qhdr, off_qring, off_stats, off_completion, off_run;
+    uint64_t off_core_shift;        // closed-loop replay: int64 per core (sum of its batch delays)
     uint64_t replica_bytes;
 };
+
+// Kernel flags (per launch).
+#define PU_KF_NOHALT   1u   // System::access semantics: no prime.cpp:130-134 stop (pu_access)
+#define PU_KF_MSGHALT  2u   // a negative running delay stops only that message's receive
+                            // thread (pu_req.tag): the rest of the message and every later
+                            // message with that tag are skipped (the server, prime.cpp:130-134
+                            // with num_recv_threads > 1)
+#define PU_KF_CLOSED   4u   // closed-loop replay: timer_i += the core's earlier batch delays
+                            // (core_manager.cpp:265 `cycle += delay` after each reply)
 
 // Per-replica run state carried across launches.
 struct RunState {
@@ -165,7 +175,9 @@ struct RunState {
                            // further request reaches the uncore
     uint64_t processed;    // requests processed so far
     int32_t pool_top;      // free entries on the sharer-bitmap pool stack
-    int32_t _pad;
+    int32_t skip_msg;      // PU_KF_MSGHALT: the open message went negative, its rest is skipped
     uint64_t page_next;    // PageTable::empty_page_num (pages allocated so far)
     uint64_t last_addr;    // address of the last request after translation (InsMem::addr_dmem)
+    int64_t msg_shift;     // PU_KF_CLOSED: the open message's core shift at its first request
+    uint64_t dead_tags;    // PU_KF_MSGHALT: receive threads (pu_req.tag < 64) that have exited
 };

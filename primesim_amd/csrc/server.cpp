@@ -35,6 +35,7 @@
 #include <deque>
 #include <list>
 #include <map>
+#include <set>
 #include <memory>
 #include <string>
 #include <utility>
@@ -42,6 +43,7 @@
 
 #include "../../include/primeuncore.h"
 #include "common.h"
+#include "geometry.h"
 
 namespace {
 
@@ -106,13 +108,15 @@ struct Conn {
 struct Msg {
     Conn* conn;
     int rank;
+    int tag;                  // MPI tag = the receive thread that takes it (prime.cpp:53)
     std::vector<MsgRec> rec;
 };
 
 // A MEM_REQUESTS message taken into this round's launch.
 struct Batch {
-    int session, rank, tag;
-    size_t first, n;   // its requests in the session's slice of the round
+    int session, rank, tag;   // tag: the reply tag (the sender's thread id)
+    int recv;                 // the receive thread (the message's MPI tag)
+    size_t first, n;          // its requests in the session's slice of the round
 };
 
 // Executor: runs a round's requests, all sessions at once.
@@ -124,6 +128,8 @@ struct Exec {
     virtual int dealloc(int s, int prog, int th) = 0;
     virtual int get(int s, int prog, int th) = 0;
     virtual std::string report(int s) = 0;
+    // PU_ERRF_LIMITS bits of session s after the last run (0: exact so far)
+    virtual uint64_t limit_flags(int) { return 0; }
 };
 
 // The product executor: the HIP engine, one wavefront per session.
@@ -161,12 +167,18 @@ struct EngineExec : Exec {
         if (hipMemcpy(d_reqs, reqs.data(), n * sizeof(pu_req), hipMemcpyHostToDevice) != hipSuccess ||
             hipMemcpy(d_off, full.data(), full.size() * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess)
             return pu::set_error(PU_EIO, "server: upload");
-        int rc = pu_run_device(h, d_reqs, d_off, d_delays, nullptr);   // on the engine's stream
+        // a negative running delay stops only that message's receive thread
+        int rc = pu::run_device_flags(h, d_reqs, d_off, d_delays, PU_KF_MSGHALT);
         if (!rc) rc = pu_synchronize(h);
         if (rc) return rc;
         if (hipMemcpy(delays, d_delays, n * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
             return pu::set_error(PU_EIO, "server: download");
-        return 0;
+        flags.assign(off.size() - 1, 0);
+        return pu_error_flags(h, flags.data(), flags.size());
+    }
+    std::vector<uint64_t> flags;
+    uint64_t limit_flags(int s) override {
+        return (size_t)s < flags.size() ? flags[(size_t)s] & PU_ERRF_LIMITS : 0;
     }
     int alloc(int s, int p, int t) override { return pu_alloc_core_replica(h, s, p, t); }
     int dealloc(int s, int p, int t) override { return pu_dealloc_core_replica(h, s, p, t); }
@@ -186,19 +198,23 @@ struct FnExec : Exec {
     pu_exec_fn fn;
     void* ctx;
     std::vector<pu::Sched> sched;
+    std::vector<uint64_t> flags;
     FnExec(pu_exec_fn f, void* c, int sessions, int cores) : fn(f), ctx(c), sched((size_t)sessions) {
         for (auto& s : sched) s.stat.assign((size_t)cores, 0);
+        flags.assign((size_t)sessions, 0);
     }
     int run(const std::vector<pu_req>& reqs, const std::vector<uint64_t>& off, int32_t* delays) override {
         for (size_t s = 0; s + 1 < off.size(); s++) {
             size_t a = off[s], b = off[s + 1];
             if (b > a) {
                 int rc = fn(ctx, (int)s, reqs.data() + a, b - a, delays + a);
-                if (rc) return rc;
+                if (rc < 0) return rc;
+                flags[s] |= (uint64_t)rc;      // > 0: PU_ERRF_* bits of that session's replica
             }
         }
         return 0;
     }
+    uint64_t limit_flags(int s) override { return flags[(size_t)s] & PU_ERRF_LIMITS; }
     int alloc(int s, int p, int t) override { return sched[(size_t)s].alloc(p, t); }
     int dealloc(int s, int p, int t) override { return sched[(size_t)s].dealloc(p, t); }
     int get(int s, int p, int t) override { return sched[(size_t)s].get(p, t); }
@@ -207,7 +223,7 @@ struct FnExec : Exec {
 
 struct Session {
     bool started = false, ended = false, halted = false;
-    int exits = 0;
+    std::set<int> done_tags;    // receive threads that returned (PROGRAM_EXITING, negative delay)
     std::list<int> prog_list;   // prime.h: list<int> prog_list
     size_t prog_count = 0;
     std::deque<Msg> backlog;
@@ -326,8 +342,9 @@ bool handle_control(pu_server* s, int si, Msg& m) {
     case kThreadFinishing:                                      // prime.cpp:110-114
         s->exec->dealloc(si, src, h.mem_size);
         return true;
-    case kProgramExiting:                                       // prime.cpp:116-118
-        if (++S.exits >= s->nthreads) end_session(s, si);
+    case kProgramExiting:                                       // prime.cpp:116-118: thread `tag` returns
+        S.done_tags.insert(m.tag);
+        if ((int)S.done_tags.size() >= s->nthreads) end_session(s, si);
         return true;
     default:
         return false;
@@ -362,7 +379,7 @@ int parse_conn(pu_server* s, Conn* c) {
             Session& S = s->sess[(size_t)c->session];
             int nrec = f.a / (int)sizeof(MsgRec);
             if (!S.ended && nrec > 0) {
-                Msg m{c, c->rank, std::vector<MsgRec>((size_t)nrec)};
+                Msg m{c, c->rank, f.tag, std::vector<MsgRec>((size_t)nrec)};
                 std::memcpy(m.rec.data(), c->in.data() + pos + sizeof f, (size_t)f.a);
                 S.started = true;
                 S.backlog.push_back(std::move(m));
@@ -451,6 +468,10 @@ int serve_round(pu_server* s, int timeout_ms) {
                           m.rec[0].timer == kThreadFinishing || m.rec[0].timer == kProgramExiting;
             if (is_ctl && mem) break;           // wait for this round's batches to finish first
             handled++;
+            if (S.done_tags.count(m.tag)) {     // its receive thread has returned: never received
+                S.backlog.pop_front();
+                continue;
+            }
             if (is_ctl) {
                 handle_control(s, si, m);
                 if (!S.ended) S.backlog.pop_front();
@@ -463,7 +484,7 @@ int serve_round(pu_server* s, int timeout_ms) {
             msg_len = std::min<int64_t>(msg_len, (int64_t)m.rec.size());
             msg_len = std::min<int64_t>(msg_len, (int64_t)s->max_msg + 1);
             const int core = s->exec->get(si, m.rank, thread_id);
-            Batch b{si, m.rank, thread_id, reqs.size() - off[(size_t)si], 0};
+            Batch b{si, m.rank, thread_id, m.tag, reqs.size() - off[(size_t)si], 0};
             for (int64_t i = 1; i < msg_len; i++) {
                 pu_req q;
                 std::memset(&q, 0, sizeof q);
@@ -473,6 +494,7 @@ int serve_round(pu_server* s, int timeout_ms) {
                 q.prog_id = m.rank;
                 q.mem_type = m.rec[(size_t)i].mem_type ? 1 : 0;
                 q.batch_start = i == 1;
+                q.tag = (uint16_t)m.tag;
                 reqs.push_back(q);
                 b.n++;
             }
@@ -491,6 +513,16 @@ int serve_round(pu_server* s, int timeout_ms) {
         for (const Batch& b : batches) {
             Session& S = s->sess[(size_t)b.session];
             if (S.ended) continue;
+            if (uint64_t lim = s->exec->limit_flags(b.session)) {
+                // an engine limit stopped the replica where the reference continues:
+                // no reply is exact from here on, end the session with an error
+                std::fprintf(stderr, "[primeuncore] session %d stopped by an engine limit (error flags 0x%llx)\n",
+                             b.session, (unsigned long long)lim);
+                s->st.sessions_failed++;
+                end_session(s, b.session);
+                continue;
+            }
+            if (S.done_tags.count(b.recv)) continue;         // an earlier batch stopped this thread
             const int32_t* d = delays.data() + off[(size_t)b.session] + b.first;
             const pu_req* q = reqs.data() + off[(size_t)b.session] + b.first;
             int32_t D = 0;
@@ -504,10 +536,11 @@ int serve_round(pu_server* s, int timeout_ms) {
                     break;
                 }
             }
-            if (neg) {
+            if (neg) {                                          // that handler thread returns, unanswered
+                S.done_tags.insert(b.recv);
+                if (!S.halted) s->st.sessions_halted++;
                 S.halted = true;
-                s->st.sessions_halted++;
-                end_session(s, b.session);
+                if ((int)S.done_tags.size() >= s->nthreads) end_session(s, b.session);
                 continue;
             }
             deliver(S, b.rank, b.tag, D);                       // prime.cpp:136
@@ -533,6 +566,10 @@ pu_server* make_server(Exec* ex, const pu_server_opts* o) {
     s->prefix = o->report_prefix ? o->report_prefix : "";
     s->nsessions = o->num_sessions > 0 ? o->num_sessions : 1;
     s->nthreads = o->num_recv_threads > 0 ? o->num_recv_threads : 1;
+    if (s->nthreads > 64) {
+        pu::set_error(PU_ENOTSUP, "server: at most 64 receive threads (the engine's per-thread stop mask)");
+        return nullptr;
+    }
     s->max_msg = o->max_msg_size > 0 ? o->max_msg_size : 100;
     s->verbose = o->verbose;
     s->sess.resize((size_t)s->nsessions);

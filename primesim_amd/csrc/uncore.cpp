@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstddef>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -30,7 +31,7 @@
 
 extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,
                                 const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
-                                uint64_t budget_ticks, hipStream_t stream);
+                                uint64_t budget_ticks, uint32_t flags, hipStream_t stream);
 extern "C" int pu_engine_init_pool(char* arena, uint64_t replica_bytes, uint64_t off_pool_free, uint64_t off_run,
                                    int pool_entries, int nreplicas, hipStream_t stream);
 extern "C" int pu_engine_unit_queue(const Geo* d_geo, char* base, uint64_t minp, const uint64_t* t,
@@ -181,7 +182,7 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
         T.idxbits = ilog2(T.nsets);
         T.access_time = tc.access_time;
         T.page_miss_delay = y.page_miss_delay;
-        uint64_t cap = 1ull << 20;
+        uint64_t cap = 1ull << 22;     // 3.1 M distinct pages (12 GiB at 4 KB) before PU_ERRF_PAGES
         if (const char* e = std::getenv("PRIMEUNCORE_PAGE_ENTRIES")) cap = std::strtoull(e, nullptr, 10);
         uint64_t p2 = 64;
         while (p2 < cap && p2 < (1ull << 32)) p2 <<= 1;
@@ -204,10 +205,15 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
     uint64_t dlines = bus_sys ? 0 : (uint64_t)N * D.csets * D.nways;
     D.off_line = lay.take(dlines * sizeof(DirLine));
     // sharer sets of more than 4 LLCs live in pool bitmaps: one entry per
-    // directory line up to 65,536 lines (it cannot run out), one per 64 lines
-    // beyond (PRIMEUNCORE_POOL_ENTRIES overrides); running out stops the
-    // replica with PU_ERRF_POOL rather than diverge
-    uint64_t pool = bus_sys ? 0 : (dlines <= 65536 ? std::max<uint64_t>(dlines, 64) : std::max<uint64_t>(dlines / 64, 65536));
+    // directory line (a line holds at most one, so the pool cannot run out)
+    // unless that exceeds 2 GiB of bitmaps; then as many as fit, and running
+    // out stops the replica with PU_ERRF_POOL rather than diverge.
+    // PRIMEUNCORE_POOL_ENTRIES overrides (tests)
+    uint64_t pool = 0;
+    if (!bus_sys) {
+        const uint64_t cap = (2ull << 30) / ((uint64_t)D.nwords * 8);
+        pool = std::max<uint64_t>(std::min(dlines, cap), 64);
+    }
     if (const char* e = std::getenv("PRIMEUNCORE_POOL_ENTRIES"); e && !bus_sys) pool = std::strtoull(e, nullptr, 10);
     if (pool > (1ull << 30)) pool = 1ull << 30;
     D.pool_entries = (int32_t)pool;
@@ -229,6 +235,7 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
     g->off_stats = lay.take(sizeof(EngineStats));
     g->off_completion = lay.take((uint64_t)y.num_cores * 8);
     g->off_run = lay.take(sizeof(RunState));
+    g->off_core_shift = lay.take((uint64_t)y.num_cores * 8);
     g->replica_bytes = align_up(lay.cur, 4096);
     return 0;
 }
@@ -245,6 +252,7 @@ struct pu_handle {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0.0;
+    uint32_t replay_flags = 0;   // PU_KF_CLOSED under PU_REPLAY_CLOSED
     // ThreadSched (thread_sched.cpp): the shared one, and per-replica copies
     // made on first use of a per-replica call (pu_*_core_replica: the server's
     // sessions); the shared calls update both
@@ -297,13 +305,39 @@ int ensure_stage(pu_handle* h, size_t n) {
 }
 
 int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
-           hipStream_t s, uint64_t* d_pos = nullptr, uint64_t budget_ticks = 0) {
+           hipStream_t s, uint64_t* d_pos = nullptr, uint64_t budget_ticks = 0, uint32_t extra_flags = 0) {
     HIP_TRY(hipEventRecord(h->ev0, s), PU_EIO);
     int rc = pu_engine_launch(h->d_geo, h->geo.num_levels, h->arena, replica0, nblocks, d_reqs, d_off, d_delay, d_pos,
-                              budget_ticks, s);
+                              budget_ticks, (extra_flags & PU_KF_NOHALT) ? extra_flags : (h->replay_flags | extra_flags),
+                              s);
     if (rc) return pu::set_error(rc, "engine launch failed");
     HIP_TRY(hipEventRecord(h->ev1, s), PU_EIO);
     return 0;
+}
+
+// Gathers EngineStats.error_flags of replicas [0, n) (one strided copy).
+int gather_error_flags(pu_handle* h, uint64_t* out, size_t n) {
+    if (n == 0) return 0;
+    const Geo& g = h->geo;
+    HIP_TRY(hipStreamSynchronize(h->stream), PU_EIO);
+    HIP_TRY(hipMemcpy2D(out, sizeof(uint64_t), h->arena + g.off_stats + offsetof(EngineStats, error_flags),
+                        g.replica_bytes, sizeof(uint64_t), n, hipMemcpyDeviceToHost), PU_EIO);
+    return 0;
+}
+
+// PU_ESTATE with a message when `flags` holds an engine-limit or undefined-
+// state bit (everything but the reference's own negative-delay stop).
+int limit_error(uint64_t flags, int replica) {
+    const uint64_t bad = flags & PU_ERRF_LIMITS;
+    if (!bad) return 0;
+    std::string m = "replica " + std::to_string(replica) + " stopped:";
+    if (bad & PU_ERRF_POOL) m += " sharer-bitmap pool exhausted (PRIMEUNCORE_POOL_ENTRIES);";
+    if (bad & PU_ERRF_PAGES) m += " page table full (PRIMEUNCORE_PAGE_ENTRIES);";
+    if (bad & PU_ERRF_PROG) m += " prog_id outside the packed directory line's range;";
+    if (bad & PU_ERRF_WB_MISS) m += " write-back missed at its home (reference NULL dereference, Q13);";
+    if (bad & PU_ERRF_EMPTY_SHARER) m += " owner lookup on an empty sharer set;";
+    if (bad & PU_ERRF_QUEUE) m += " queue-model precondition violated;";
+    return pu::set_error(PU_ESTATE, m);
 }
 
 // Copies replica r's engine-side counters.
@@ -360,7 +394,27 @@ void cache_report(std::ostream& o, uint64_t size, uint64_t ways, const uint64_t*
 extern "C" {
 
 const char* pu_last_error(void) { return pu::g_err.c_str(); }
-const char* pu_version(void) { return "primeuncore 0.1 (gfx950)"; }
+#ifndef PU_SRC_HASH
+#define PU_SRC_HASH "unknown"
+#endif
+// The source hash (tools/src_hash.py over primesim_amd/csrc and include/) the
+// library was built from: tests and smoke() compare it with the checkout.
+const char* pu_version(void) { return "primeuncore 0.2 (gfx950) src " PU_SRC_HASH; }
+
+int pu_set_replay_mode(pu_handle* h, int mode) {
+    if (!h) return pu::set_error(PU_EINVAL, "null handle");
+    if (mode != PU_REPLAY_OPEN && mode != PU_REPLAY_CLOSED) return pu::set_error(PU_EINVAL, "unknown replay mode");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->replay_flags = mode == PU_REPLAY_CLOSED ? PU_KF_CLOSED : 0u;
+    return 0;
+}
+
+int pu_error_flags(pu_handle* h, uint64_t* out, size_t n) {
+    if (!h || (!out && n)) return pu::set_error(PU_EINVAL, "bad arguments");
+    if (n > (size_t)h->R) return pu::set_error(PU_ERANGE, "more replicas than the handle holds");
+    std::lock_guard<std::mutex> lk(h->mu);
+    return gather_error_flags(h, out, n);
+}
 
 pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device) {
     if (!cfg || num_replicas < 1) {
@@ -495,7 +549,8 @@ int pu_get_core_id_replica(pu_handle* h, int replica, int prog_id, int thread_id
     return s->get(prog_id, thread_id);
 }
 
-int pu_access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n, int32_t* delay_out) {
+namespace {
+int access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n, int32_t* delay_out, uint32_t extra) {
     if (!h || (!reqs && n)) return pu::set_error(PU_EINVAL, "bad arguments");
     if (replica < 0 || replica >= h->R) return pu::set_error(PU_ERANGE, "replica out of range");
     if (n == 0) return 0;
@@ -505,14 +560,25 @@ int pu_access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n, int
     uint64_t off[2] = {0, (uint64_t)n};
     HIP_TRY(hipMemcpyAsync(h->d_reqs, reqs, n * sizeof(pu_req), hipMemcpyHostToDevice, h->stream), PU_EIO);
     HIP_TRY(hipMemcpyAsync(h->d_off, off, sizeof(off), hipMemcpyHostToDevice, h->stream), PU_EIO);
-    rc = launch(h, replica, 1, h->d_reqs, h->d_off, h->d_delays, h->stream);
+    rc = launch(h, replica, 1, h->d_reqs, h->d_off, h->d_delays, h->stream, nullptr, 0, extra);
     if (rc) return rc;
     if (delay_out)
         HIP_TRY(hipMemcpyAsync(delay_out, h->d_delays, n * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream), PU_EIO);
+    uint64_t ef = 0;
+    HIP_TRY(hipMemcpyAsync(&ef, h->arena + (size_t)replica * h->geo.replica_bytes + h->geo.off_stats +
+                                    offsetof(EngineStats, error_flags),
+                           sizeof(ef), hipMemcpyDeviceToHost, h->stream), PU_EIO);
     HIP_TRY(hipStreamSynchronize(h->stream), PU_EIO);
     float ms = 0;
     if (hipEventElapsedTime(&ms, h->ev0, h->ev1) == hipSuccess) h->last_ms = ms;
-    return 0;
+    // an engine limit stopped the replica where the reference would continue:
+    // the delays after that request are not the reference's, say so
+    return limit_error(ef, replica);
+}
+}  // namespace
+
+int pu_access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n, int32_t* delay_out) {
+    return access_batch(h, replica, reqs, n, delay_out, 0);
 }
 
 int pu_access(pu_handle* h, int core_id, int prog_id, int mem_type, uint64_t* addr, int64_t timer) {
@@ -527,7 +593,9 @@ int pu_access(pu_handle* h, int core_id, int prog_id, int mem_type, uint64_t* ad
     r.mem_type = (uint8_t)mem_type;
     r.batch_start = 1;   // a lone request: running delay 0, `timer` used as given
     int32_t d = 0;
-    int rc = pu_access_batch(h, 0, &r, 1, &d);
+    // UncoreManager::uncore_access has no prime.cpp halt rule (PU_KF_NOHALT); a
+    // closed-loop shift would move the caller's timer, so it is never applied here
+    int rc = access_batch(h, 0, &r, 1, &d, PU_KF_NOHALT);
     if (rc) return rc;
     if (h->geo.tlb_enable) {    // InsMem::addr_dmem now holds the physical address (system.cpp:916)
         RunState rs;
@@ -543,6 +611,17 @@ int pu_run_device(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int
     std::lock_guard<std::mutex> lk(h->mu);
     return launch(h, 0, h->R, d_reqs, d_off, d_delay, s);
 }
+
+}  // extern "C"
+
+int pu::run_device_flags(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
+                         uint32_t extra_flags) {
+    if (!h || !d_reqs || !d_off || !d_delay) return pu::set_error(PU_EINVAL, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    return launch(h, 0, h->R, d_reqs, d_off, d_delay, h->stream, nullptr, 0, extra_flags);
+}
+
+extern "C" {
 
 int pu_run_device_sliced(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
                          uint64_t* d_pos, uint64_t budget_us, void* hip_stream) {

@@ -56,7 +56,8 @@ class PrimeServer:
     @classmethod
     def with_executor(cls, fn: Callable[[int, np.ndarray], np.ndarray], num_cores: int, socket_path: str,
                       sessions: int = 1, recv_threads: int = 1, max_msg: int = 100) -> "PrimeServer":
-        """Protocol-test server: fn(session, reqs) -> per-request delays, on the host."""
+        """Protocol-test server: fn(session, reqs) -> per-request delays (or
+        (delays, PU_ERRF_* bits) to report an engine-side error), on the host."""
         self = cls.__new__(cls)
 
         def tramp(_ctx, session, reqs_p, n, delays_p):
@@ -64,8 +65,12 @@ class PrimeServer:
                 reqs = np.frombuffer((C.c_char * (n * A.REQ_DTYPE.itemsize)).from_address(reqs_p),
                                      dtype=A.REQ_DTYPE).copy()
                 out = np.frombuffer((C.c_int32 * n).from_address(delays_p), dtype=np.int32)
-                out[:] = np.asarray(fn(session, reqs), dtype=np.int32)
-                return 0
+                res = fn(session, reqs)
+                flags = 0
+                if isinstance(res, tuple):
+                    res, flags = res
+                out[:] = np.asarray(res, dtype=np.int32)
+                return int(flags)
             except Exception:   # noqa: BLE001 — reported to the C side as an error code
                 return -5
 

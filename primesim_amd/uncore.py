@@ -67,6 +67,8 @@ def lib() -> C.CDLL:
         "pu_last_kernel_ms": (C.c_double, [C.c_void_p]),
         "pu_last_error": (C.c_char_p, []),
         "pu_version": (C.c_char_p, []),
+        "pu_set_replay_mode": (C.c_int, [C.c_void_p, C.c_int]),
+        "pu_error_flags": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
         "pu_stream_count": (C.c_int64, [P(A.StreamParams)]),
         "pu_stream_generate": (C.c_int64, [P(A.StreamParams), C.c_void_p, C.c_size_t]),
         "pu_stream_thread_of": (C.c_int, [P(A.StreamParams), C.c_int, P(C.c_int), P(C.c_int)]),
@@ -114,6 +116,18 @@ def lib() -> C.CDLL:
 
 def last_error() -> str:
     return lib().pu_last_error().decode()
+
+
+# PU_E* codes (include/primeuncore.h); any other negative pu_access value is a
+# delay that wrapped in the reference's `int`
+PU_ERRORS = (-5, -12, -19, -22, -34, -71, -95)
+PU_REPLAY_OPEN, PU_REPLAY_CLOSED = 0, 1
+
+
+def library_source_hash() -> str:
+    """The source hash pu_version() was built with (tools/src_hash.py)."""
+    v = lib().pu_version().decode()
+    return v.rsplit(" src ", 1)[1] if " src " in v else ""
 
 
 # ---------------------------------------------------------------- config
@@ -370,7 +384,7 @@ class UncoreManager:
     def uncore_access(self, core_id: int, ins_mem: InsMem, timer: int) -> int:
         addr = C.c_uint64(ins_mem.addr_dmem)
         d = lib().pu_access(self._handle(), core_id, ins_mem.prog_id, ins_mem.mem_type, C.byref(addr), timer)
-        if d < -1:
+        if d in PU_ERRORS:
             raise UncoreError(f"uncore_access: {last_error()}")
         ins_mem.addr_dmem = addr.value
         return d
@@ -382,6 +396,20 @@ class UncoreManager:
         rc = lib().pu_access_batch(self._handle(), replica, reqs.ctypes.data, len(reqs), out.ctypes.data)
         if rc != 0:
             raise UncoreError(f"access_batch: {last_error()}")
+        return out
+
+    def set_replay_mode(self, mode: int) -> None:
+        """PU_REPLAY_OPEN (recorded timers) or PU_REPLAY_CLOSED (timer_i += the
+        core's earlier batch delays, core_manager.cpp:265)."""
+        if lib().pu_set_replay_mode(self._handle(), mode) != 0:
+            raise UncoreError(last_error())
+
+    def error_flags(self, n: Optional[int] = None) -> np.ndarray:
+        """PU_ERRF_* bits of replicas [0, n)."""
+        n = self.replicas if n is None else n
+        out = np.zeros(n, dtype=np.uint64)
+        if lib().pu_error_flags(self._handle(), out.ctypes.data, n) != 0:
+            raise UncoreError(last_error())
         return out
 
     def run_device(self, d_reqs_ptr: int, d_off_ptr: int, d_delay_ptr: int, stream_ptr: int = 0) -> None:

@@ -2,6 +2,7 @@
 the reference's own uncore) and to read the reference's report text."""
 from __future__ import annotations
 
+import hashlib
 import json
 import os
 import re
@@ -13,25 +14,69 @@ from primesim_amd import _abi as A
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def case_names() -> list[str]:
+def _all_names() -> list[str]:
     return sorted(f[:-5] for f in os.listdir(GOLDEN) if f.endswith(".json") and f not in
                   ("network.json", "configs.json"))
+
+
+def case_names() -> list[str]:
+    """Fixtures that hold their requests and every delay."""
+    return [n for n in _all_names() if not n.startswith("big_")]
+
+
+def big_case_names() -> list[str]:
+    """Full-size preset runs stored as digests (requests regenerate from the spec)."""
+    return [n for n in _all_names() if n.startswith("big_")]
+
+
+def sha256(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).view(np.uint8).tobytes()).hexdigest()
 
 
 class Case:
     def __init__(self, name: str):
         self.name = name
         z = np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False)
-        self.reqs = z["reqs"].view(A.REQ_DTYPE)
-        self.delays = z["delays"]
+        with open(os.path.join(GOLDEN, f"{name}.json")) as f:
+            self.meta = json.load(f)
+        self.digest = self.meta.get("digest")
+        if self.digest:
+            import primesim_amd as P
+            spec = P.StreamSpec(**self.meta["stream"])
+            self.reqs = P.generate_stream(spec)
+            assert sha256(self.reqs) == self.digest["reqs_sha256"], f"{name}: stream generator drifted"
+            self.delays = None
+            self.head, self.tail = z["head"], z["tail"]
+        else:
+            self.reqs = z["reqs"].view(A.REQ_DTYPE)
+            self.delays = z["delays"]
         self.completion = z["completion"]
         self.xml_path = os.path.join(GOLDEN, f"{name}.xml")
         with open(os.path.join(GOLDEN, f"{name}.report.txt")) as f:
             self.report = f.read()
-        with open(os.path.join(GOLDEN, f"{name}.json")) as f:
-            self.meta = json.load(f)
         self.threads = [tuple(t) for t in self.meta["threads"]]
         self.counters = self.meta["counters"]
+        self.closed = self.meta.get("replay", "open") == "closed"
+
+    def check_delays(self, d: np.ndarray) -> None:
+        """Every delay equals the reference's (in full, or by digest)."""
+        if self.delays is not None:
+            np.testing.assert_array_equal(d, self.delays)
+            return
+        np.testing.assert_array_equal(d[:len(self.head)], self.head)
+        np.testing.assert_array_equal(d[-len(self.tail):], self.tail)
+        assert int(d.astype(np.int64).sum()) == self.digest["delay_sum"], f"{self.name}: delay sum differs"
+        assert sha256(d.astype(np.int32)) == self.digest["delays_sha256"], f"{self.name}: delay digest differs"
+
+
+def extended_stream(case: "Case", n: int) -> np.ndarray:
+    """The case's stream regenerated with n requests (its fixture holds a prefix)."""
+    import primesim_amd as P
+    spec = dict(case.meta["stream"])
+    spec["max_requests"] = n
+    r = P.generate_stream(P.StreamSpec(**spec))
+    assert np.array_equal(r[:len(case.reqs)], case.reqs), f"{case.name}: stream generator drifted"
+    return r
 
 
 def report_stats(text: str) -> dict:

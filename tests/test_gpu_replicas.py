@@ -136,29 +136,20 @@ def test_core_out_of_range():
         um.close()
 
 
-def test_prog_id_limit_of_packed_directory_lines():
-    """Directory lines hold the program id in 10 bits: ids up to 1023 run
-    exactly; a request with another id stops the replica there with
-    PU_ERRF_PROG (it could not be stored), never a silently wrong result."""
+def test_any_prog_id_runs_exactly():
+    """Directory lines hold the whole int prog_id (InsMem::prog_id): large and
+    mixed program ids run exactly (the 0.1 engine packed 10 bits and stopped)."""
     cfg = P.config_from_dict(CF.preset("C1"))
     spec = P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 16, seed=23, max_requests=600)
     reqs = P.generate_stream(spec)
     hi = reqs.copy()
-    hi["prog_id"] = 1023
+    hi["prog_id"] = np.where(np.arange(len(hi)) % 3 == 0, 2**31 - 1, 1024 + (np.arange(len(hi)) % 5))
     um = P.UncoreManager()
     um.init(cfg)
     try:
         want, _ = _oracle_run(cfg, spec, hi)
         np.testing.assert_array_equal(um.access_batch(hi), want)
         assert um.stats().error_flags == 0
-        um.reset()
-        bad = reqs.copy()
-        bad["prog_id"][300] = 1024
-        d = um.access_batch(bad)
-        want, _ = _oracle_run(cfg, spec, reqs)
-        np.testing.assert_array_equal(d[:300], want[:300])
-        assert not d[300:].any()
-        assert um.stats().error_flags & A.PU_ERRF_PROG
     finally:
         um.close()
 

@@ -12,20 +12,21 @@ import pytest
 import oracle as O
 import primesim_amd as P
 from primesim_amd import _abi as A
-from golden_util import Case, assert_stats_match, case_names
+from golden_util import Case, assert_stats_match, big_case_names, case_names
 
 
-@pytest.mark.parametrize("name", case_names())
+@pytest.mark.parametrize("name", case_names() + big_case_names())
 def test_oracle_reproduces_reference(name):
     c = Case(name)
     cfg = P.load_config(c.xml_path)
     ref = O.CpuRef(cfg)
+    ref.set_mode(O.MODE_CLOSED if c.closed else 0)
     for prog, th in c.threads:
         ref.alloc_core(prog, th)
     d, rc = ref.run(c.reqs)
     halt = c.meta.get("halt_index")
     assert rc == (0 if halt is None else halt + 1)
-    np.testing.assert_array_equal(d, c.delays)
+    c.check_delays(d)
     np.testing.assert_array_equal(ref.completion(), c.completion)
     st = ref.stats().as_dict()
     assert st["error_flags"] == (0 if halt is None else A.PU_ERRF_NEG_DELAY)

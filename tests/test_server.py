@@ -222,3 +222,86 @@ def test_golden_replay_through_server_with_oracle_executor(tmp_path):
     starts = np.nonzero(case.reqs["batch_start"])[0].tolist() + [len(case.reqs)]
     want = [int((case.delays[a:b].astype(np.int64) - 1).sum()) for a, b in zip(starts[:-1], starts[1:])]
     assert got.tolist() == want
+
+
+def _msg_reqs(core: int, n: int, base: int, timer0: int = 0) -> np.ndarray:
+    r = np.zeros(n, P._abi.REQ_DTYPE)
+    r["addr"] = base + 64 * np.arange(n)
+    r["timer"] = timer0 + np.arange(n)
+    r["core"] = core
+    r["batch_start"][0] = 1
+    return r
+
+
+def test_negative_delay_stops_only_its_receive_thread(tmp_path):
+    """num_recv_threads = 2: a negative batch delay ends handler thread `tag`
+    only (prime.cpp:130-134 returns from msgHandler); the other thread keeps
+    serving, later messages on the dead tag are never received, and the session
+    ends once PROGRAM_EXITING has reached the surviving thread."""
+    seen = []
+    KILL = 0x7000
+
+    def ex(session, r):
+        seen.append(r.copy())
+        d = np.full(len(r), 5, np.int32)
+        d[r["addr"] == KILL] = -1000          # the running delay goes negative here
+        return d
+
+    path = _sock(tmp_path)
+    srv = S.PrimeServer.with_executor(ex, num_cores=4, socket_path=path, recv_threads=2)
+    srv.start()
+    c = S.Client(path, 0, 1)
+    c.control(P.uncore.MSG_PROCESS_STARTING)
+    tags = {}
+    for t in range(2):
+        c.control(P.uncore.MSG_NEW_THREAD, mem_size=t, tag=0)
+        tags[t] = c.recv(t)
+    assert tags == {0: 0, 1: 1}                               # core % num_recv_threads
+    # thread 1's message goes negative at its 3rd request: no reply, rest skipped
+    bad = _msg_reqs(1, 6, 0x6F80)
+    assert (bad["addr"] == KILL).sum() == 1
+    c.send(S.mem_message(1, bad), tag=1)
+    # thread 0 is still served
+    ok = _msg_reqs(0, 4, 0x100000)
+    c.send(S.mem_message(0, ok), tag=0)
+    assert c.recv(0) == 4 * (5 - 1)
+    # a later message on the dead tag is never received by anyone
+    late = _msg_reqs(1, 3, 0x200000)
+    c.send(S.mem_message(1, late), tag=1)
+    ok2 = _msg_reqs(0, 2, 0x300000)
+    c.send(S.mem_message(0, ok2), tag=0)
+    assert c.recv(0) == 2 * (5 - 1)
+    c.control(P.uncore.MSG_PROGRAM_EXITING, tag=0)
+    assert srv.join(10) == 0
+    st = srv.stats()
+    assert st["sessions_halted"] == 1 and st["sessions_ended"] == 1 and st["sessions_failed"] == 0
+    executed = np.concatenate(seen)
+    assert not np.isin(late["addr"], executed["addr"]).any()
+    c.close()
+    srv.close()
+
+
+def test_engine_limit_ends_session_without_reply(tmp_path):
+    """An engine-side limit (PU_ERRF_LIMITS, e.g. the sharer pool) means no
+    exact reply exists: the session ends with an error instead of replying."""
+    def ex(session, r):
+        d = np.full(len(r), 3, np.int32)
+        return (d, P._abi.PU_ERRF_POOL) if (r["addr"] == 0xBAD0).any() else d
+
+    path = _sock(tmp_path)
+    srv = S.PrimeServer.with_executor(ex, num_cores=2, socket_path=path)
+    srv.start()
+    c = S.Client(path, 0, 1)
+    c.control(P.uncore.MSG_PROCESS_STARTING)
+    c.control(P.uncore.MSG_NEW_THREAD, mem_size=0, tag=0)
+    assert c.recv(0) == 0
+    c.send(S.mem_message(0, _msg_reqs(0, 3, 0x1000)), tag=0)
+    assert c.recv(0) == 3 * 2
+    c.send(S.mem_message(0, _msg_reqs(0, 3, 0xBAD0 - 64)), tag=0)
+    with pytest.raises(UncoreError):
+        c.recv(0)                                             # EOF: no reply for a wrong delay
+    assert srv.join(10) == 0
+    st = srv.stats()
+    assert st["sessions_failed"] == 1 and st["sessions_ended"] == 1
+    c.close()
+    srv.close()

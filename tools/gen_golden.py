@@ -141,6 +141,25 @@ def cases() -> dict:
                             S(A.PU_STREAM_MULTIPROGRAM, 16, seed=27, num_quanta=1, num_progs=2))
     c["bus_c2"] = (CF.preset("C2", sys_type=1), S(A.PU_STREAM_SHARED_UNIFORM, 64, seed=29, num_quanta=1,
                                                   max_requests=20000))
+    # closed-loop replay (timer_i += the core's earlier batch delays, core_manager.cpp:265)
+    c["c1_closed"] = (CF.preset("C1"), S(A.PU_STREAM_UNIFORM_HOTSPOT, 16, seed=31, num_quanta=4), {"replay": "closed"})
+    c["c3_closed"] = (CF.preset("C3"), S(A.PU_STREAM_MULTIPROGRAM, 256, seed=33, num_quanta=1, num_progs=4,
+                                         max_requests=20000), {"replay": "closed"})
+    c["c4_closed"] = (CF.preset("C4"), S(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=34, quantum=40, num_quanta=2,
+                                         max_requests=30000), {"replay": "closed"})
+    # full-size runs at the presets, stored as digests (requests regenerate from
+    # the stream spec; delays by sha256, completion cycles and report in full)
+    c["big_c4_quantum"] = (CF.preset("C4"), S(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=4, num_quanta=1),
+                           {"digest": True})
+    c["big_c4_closed"] = (CF.preset("C4"), S(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=404, num_quanta=1),
+                          {"digest": True, "replay": "closed"})
+    c["big_c3"] = (CF.preset("C3"), S(A.PU_STREAM_MULTIPROGRAM, 256, seed=303, num_quanta=1, num_progs=4),
+                   {"digest": True})
+    # open loop: a queue delay wraps the reference's int at request 165,860 (halt)
+    c["big_c5_preset"] = (CF.preset("C5"), S(A.PU_STREAM_PRODUCER_CONSUMER, 4096, seed=505, num_quanta=1),
+                          {"digest": True})
+    c["big_c5_closed"] = (CF.preset("C5"), S(A.PU_STREAM_PRODUCER_CONSUMER, 4096, seed=505, num_quanta=1),
+                          {"digest": True, "replay": "closed"})
     return c
 
 
@@ -154,7 +173,14 @@ def cfg_dict(cfg: A.SimCfg) -> dict:
     return conv(cfg)
 
 
-def gen_case(name: str, sim: dict, spec: P.StreamSpec) -> None:
+def sha256(a: np.ndarray) -> str:
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).view(np.uint8).tobytes()).hexdigest()
+
+
+def gen_case(name: str, sim: dict, spec: P.StreamSpec, opts: dict | None = None) -> None:
+    opts = opts or {}
+    mode = O.MODE_CLOSED if opts.get("replay") == "closed" else 0
     xml = CF.to_xml(sim)
     with tempfile.NamedTemporaryFile("w", suffix=".xml", delete=False) as f:
         f.write(xml)
@@ -164,6 +190,7 @@ def gen_case(name: str, sim: dict, spec: P.StreamSpec) -> None:
     # screen with the CPU restatement first: states the reference treats as
     # undefined (e.g. Q13's NULL dereference) would crash the generator
     pre = O.CpuRef(P.load_config(path))
+    pre.set_mode(mode)
     for prog, th in threads:
         pre.alloc_core(prog, th)
     pre.run(reqs)
@@ -171,6 +198,7 @@ def gen_case(name: str, sim: dict, spec: P.StreamSpec) -> None:
         raise SystemExit(f"{name}: stream reaches a reference-undefined state (flags {pre.stats().error_flags})")
     pre.close()
     ref = O.RefUncore(path)
+    ref.set_mode(mode)
     for prog, th in threads:
         ref.alloc_core(prog, th)
     delays, rc = ref.run(reqs)
@@ -190,9 +218,17 @@ def gen_case(name: str, sim: dict, spec: P.StreamSpec) -> None:
         "halt_index": halt_index,
         "xmlsim": parsed,
         "generator": "tools/gen_golden.py via oracle/_ref/libprime_ref.so (reference src compiled in place)",
+        "replay": opts.get("replay", "open"),
+        "requests": int(len(reqs)),
     }
-    np.savez_compressed(os.path.join(GOLDEN, f"{name}.npz"), reqs=reqs.view(np.uint8), delays=delays,
-                        completion=comp)
+    if opts.get("digest"):
+        meta["digest"] = {"reqs_sha256": sha256(reqs), "delays_sha256": sha256(delays.astype(np.int32)),
+                          "delay_sum": int(delays.astype(np.int64).sum())}
+        np.savez_compressed(os.path.join(GOLDEN, f"{name}.npz"), completion=comp, head=delays[:2000],
+                            tail=delays[-2000:])
+    else:
+        np.savez_compressed(os.path.join(GOLDEN, f"{name}.npz"), reqs=reqs.view(np.uint8), delays=delays,
+                            completion=comp)
     with open(os.path.join(GOLDEN, f"{name}.xml"), "w") as f:
         f.write(xml)
     with open(os.path.join(GOLDEN, f"{name}.report.txt"), "w") as f:
@@ -284,9 +320,10 @@ def main() -> None:
         sys.exit("oracle/_ref/libprime_ref.so missing: run `make -C oracle ref` (needs /root/reference)")
     os.makedirs(GOLDEN, exist_ok=True)
     only = set(sys.argv[1:])
-    for name, (sim, spec) in cases().items():
-        if not only or name in only:
-            gen_case(name, sim, spec)
+    for name, case in cases().items():
+        big = len(case) > 2 and case[2].get("digest")
+        if (not only and not big) or name in only or (big and "big" in only):
+            gen_case(name, *case)
     if not only or "queue" in only:
         gen_queue()
     if not only or "network" in only:
