@@ -7,28 +7,37 @@ DRAM 120 cycles; synthetic stream: 80% uniform over 2^20 lines + 20% over a
 64-line hotspot, 25% writes, 1-4-cycle gaps, 1000-cycle barriers,
 100-request messages, canonical order.
 
-Every replica on this GPU first runs the first quantum of its own request
-stream untimed, in --warmup fixed steps of --chunk (40,960) requests (a C4
-quantum is ~409,600 requests: 1024 cores x ~400 requests per 1000-cycle
-quantum, so every core is active; cold caches and empty link histories).  The
-requests of the next --steps x --chunk are then made resident in HBM and each
-timed "step" is one engine launch (the hot path: prime.cpp's message loop over
-System::access) in which every replica continues its own stream for a
---slice-ms wall-time slice, stopping only between requests
-(pu_run_device_sliced).  Replicas differ several-fold in cost per request (link
-histories, tree-vs-M/G/1 mix), so a fixed number of requests per replica per
-launch would leave most waves idle behind the slowest (measured 26% busy); the
-slice keeps every wave simulating.  A replica is one complete, independent
-1024-core uncore (its own seed); the engine runs one replica per wavefront and
-many replicas per GPU, because a single uncore is a strictly sequential fold
-(DESIGN.md).  `value` = all requests processed by all ranks / max-over-ranks
-wall time of the K timed steps.  --slice-ms 0 gives fixed --chunk steps.
+Headline (`value`): every replica on this GPU first runs --warmup fixed steps
+of --chunk (40,960) requests of its own stream untimed (a C4 quantum is
+~409,600 requests: 1024 cores x ~400 requests per 1000-cycle quantum, so every
+core is active; cold caches and empty link histories are warmed).  The next
+--steps x --chunk requests are then made resident in HBM and each timed "step"
+is one engine launch (prime.cpp's message loop over System::access) in which
+every replica continues its own stream for a --slice-ms wall-time slice,
+stopping only between requests (pu_run_device_sliced): replicas differ
+several-fold in cost per request, and the slice keeps every wave simulating.
+A replica is one complete, independent 1024-core uncore (its own seed), one
+per wavefront.  `value` = all requests processed by all ranks / max-over-ranks
+wall time of the K timed steps.  Replay is open loop (recorded timers).
 
-Rank 0 also times the reference's own CPU uncore (oracle/_ref, compiled from
-/root/reference in the build container) — or, if that library is absent, the
-CPU restatement — on replica 0's stream on one host core: an untimed fill over
-the warmup requests, then timed over the GPU's timed window; it checks that the
-GPU's delays for every request it ran are bit-identical.
+At N=1 (rank 0) the same line also carries:
+  * per_simulation_accesses_per_s — value / replicas: the rate of ONE of the
+    concurrent simulations;
+  * single_instance — ONE simulation alone on the GPU (a 1-replica engine on
+    replica 0's stream, same warmup, then --single-requests in one launch);
+  * closed_loop — the same workload replayed closed-loop (timer_i += the core's
+    earlier batch delays, core_manager.cpp:265): rate, halted replicas, M/G/1
+    share, parity vs the reference in closed mode;
+  * cpu_baseline — the reference's own uncore (oracle/_ref) on ONE host core
+    on replica 0's stream (untimed fill over the warmup, then the GPU's timed
+    window), with bit-exact parity of every delay both ran;
+  * cpu_baseline_ensemble — the reference on ALL host cores of this box's
+    share, one replica per process (forked before any GPU call), each on its
+    replica's stream after the same fill: the ensemble comparison.
+  * roofline.traffic — fabric bytes (FETCH_SIZE + WRITE_SIZE, separate PMC
+    passes; includes Infinity-Cache hits) measured by tools/pmc_traffic.py for
+    THIS library build only (refused when its source hash differs).
+The run exits non-zero when a parity check fails.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 under
 torch.distributed.run (one process per GPU).
@@ -38,6 +47,7 @@ from __future__ import annotations
 import argparse
 import json
 import math
+import multiprocessing as mp
 import os
 import sys
 import tempfile
@@ -53,6 +63,7 @@ LAST_PER_REPLICA = None  # per-replica stat deltas of the timed steps (profiling
 METRIC = "simulated memory accesses/sec (uncore) at 1024 cores; % HBM roofline"
 REQ_BYTES = 32          # sizeof(pu_req)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+SEED_BASE = 4
 
 
 def log(*a):
@@ -84,12 +95,45 @@ def sum_stats(um, replicas: int) -> dict:
     return tot
 
 
-def cpu_baseline(cfg_xml: str, cfg, reqs: np.ndarray, threads, fill: int, budget_s: float):
-    """Time the reference CPU uncore (or the restatement) on reqs[fill:], after
-    an untimed run over reqs[:fill]; returns every delay it produced."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_core_share() -> int:
+    """Host cores this job may use: the box exports its CPU share in
+    OMP_NUM_THREADS (os.cpu_count() shows the whole machine there)."""
+    n = os.cpu_count() or 1
+    e = os.environ.get("OMP_NUM_THREADS")
+    if e and e.isdigit() and int(e) > 0:
+        n = min(n, int(e))
+    return n
+
+
+def stream_spec(seed: int, n: int = 0):
+    import primesim_amd as P
+    from primesim_amd import _abi as A
+    return P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=seed, num_quanta=64, max_requests=n)
+
+
+def reference_engine(cfg_xml: str, cfg, mode: int = 0):
     import oracle as O
     kind = "reference" if O.ref_available() else "port"
     eng = O.RefUncore(cfg_xml) if kind == "reference" else O.CpuRef(cfg)
+    eng.set_mode(mode)
+    return kind, eng
+
+
+def cpu_baseline(cfg_xml: str, cfg, reqs: np.ndarray, threads, fill: int, budget_s: float, mode: int = 0):
+    """Time the reference CPU uncore (or the restatement) on reqs[fill:], after
+    an untimed run over reqs[:fill]; returns every delay it produced."""
+    kind, eng = reference_engine(cfg_xml, cfg, mode)
     for prog, th in threads:
         eng.alloc_core(prog, th)
     chunk = 8192
@@ -107,34 +151,264 @@ def cpu_baseline(cfg_xml: str, cfg, reqs: np.ndarray, threads, fill: int, budget
     return kind, done - fill, el, np.concatenate(delays) if delays else np.zeros(0, np.int32)
 
 
+# ---------------------------------------------------------------- CPU ensemble
+def _ensemble_worker(conn, cfg_xml: str, seed: int, fill: int, n_timed: int, budget_s: float) -> None:
+    """One replica of the ensemble: fill untimed, wait for "go", run for budget_s."""
+    try:
+        import primesim_amd as P
+        cfg = P.load_config(cfg_xml)
+        reqs = P.generate_stream(stream_spec(seed, fill + n_timed))
+        threads = P.stream_threads(stream_spec(seed))
+        kind, eng = reference_engine(cfg_xml, cfg)
+        for prog, th in threads:
+            eng.alloc_core(prog, th)
+        for a in range(0, fill, 16384):
+            eng.run(reqs[a:min(fill, a + 16384)])
+        conn.send(("ready", kind))
+        conn.recv()                                   # go
+        done, t0 = fill, time.perf_counter()
+        while done < len(reqs) and time.perf_counter() - t0 < budget_s:
+            d, _ = eng.run(reqs[done:done + 2048])
+            done += len(d)
+        conn.send(("done", done - fill, time.perf_counter() - t0))
+    except Exception as e:  # noqa: BLE001 — reported to the parent
+        conn.send(("error", repr(e)))
+    finally:
+        conn.close()
+
+
+class Ensemble:
+    """The reference uncore on every host core of this job's share, one replica
+    per process, forked before the parent touches the GPU."""
+
+    def __init__(self, cfg_xml: str, workers: int, fill: int, n_timed: int, budget_s: float):
+        ctx = mp.get_context("fork")
+        self.workers, self.budget = workers, budget_s
+        self.fill = fill
+        self.pipes, self.procs = [], []
+        for w in range(workers):
+            a, b = ctx.Pipe()
+            p = ctx.Process(target=_ensemble_worker, args=(b, cfg_xml, SEED_BASE + w, fill, n_timed, budget_s),
+                            daemon=True)
+            p.start()
+            self.pipes.append(a)
+            self.procs.append(p)
+
+    def run(self) -> dict:
+        kinds = set()
+        for c in self.pipes:
+            msg = c.recv()
+            if msg[0] == "error":
+                raise RuntimeError(f"ensemble worker: {msg[1]}")
+            kinds.add(msg[1])
+        t0 = time.perf_counter()
+        for c in self.pipes:
+            c.send("go")
+        res = [c.recv() for c in self.pipes]
+        wall = time.perf_counter() - t0
+        for p in self.procs:
+            p.join(30)
+        bad = [r for r in res if r[0] != "done"]
+        if bad:
+            raise RuntimeError(f"ensemble worker: {bad[0]}")
+        n = sum(r[1] for r in res)
+        el = max(r[2] for r in res)
+        kind = kinds.pop() if len(kinds) == 1 else "mixed"
+        return {"value": n / el, "unit": "accesses/s", "cores": self.workers, "kind": kind,
+                "cpu_model": cpu_model(),
+                "sample": f"{self.workers} processes, one per host core of this job's share, each the "
+                          f"{'reference uncore compiled from /root/reference/src' if kind == 'reference' else kind} "
+                          f"on GPU replica w's C4 stream (w = 0..{self.workers - 1}) after an untimed "
+                          f"{self.fill}-request fill, run concurrently for {self.budget:g} s: {n} requests in "
+                          f"{el:.2f} s (wall {wall:.2f} s)",
+                "per_process_accesses_per_s": [r[1] / r[2] for r in res]}
+
+
+# ---------------------------------------------------------------- GPU passes
+class Pass:
+    """One warmup + timed run of every replica on this GPU."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, steps: int, keep_rep0: bool):
+    import torch
+    import torch.distributed as dist
+
+    import primesim_amd as P
+    from primesim_amd import _abi as A
+    from primesim_amd.dist import replica_seed
+
+    sptr = stream.cuda_stream
+    um.set_replay_mode(replay)
+    specs = [stream_spec(replica_seed(SEED_BASE, rank, r)) for r in range(R)]
+    gen = P.StreamSet(specs)
+    host = np.zeros((R, args.chunk), dtype=A.REQ_DTYPE)
+    offs = torch.from_numpy((np.arange(R + 1, dtype=np.uint64) * np.uint64(args.chunk)).view(np.int64)).to(dev)
+    rep0 = []
+
+    def next_chunk() -> torch.Tensor:
+        got = gen.next_into(host)
+        assert got == args.chunk, (got, args.chunk)
+        return torch.from_numpy(host.view(np.uint8).reshape(-1)).to(dev)
+
+    d_warm_delay = torch.zeros(R * args.chunk, dtype=torch.int32, device=dev)
+    t_w = time.time()
+    for s in range(args.warmup):
+        d_req = next_chunk()
+        um.run_device(d_req.data_ptr(), offs.data_ptr(), d_warm_delay.data_ptr(), sptr)
+        torch.cuda.synchronize(dev)
+        if keep_rep0:
+            rep0.append(d_warm_delay[:args.chunk].cpu().numpy())
+        del d_req
+        log(f"[bench] {'closed' if replay else 'open'}-loop warmup step {s} done ({time.time() - t_w:.1f}s)")
+    if os.environ.get("PU_PROF_RESET_AFTER_WARMUP"):   # tools/prof_regions.py: count the timed steps only
+        P.uncore.lib().pu_engine_prof_read(None, 0, 1)
+    t_gen = time.time()
+    W_t = steps * args.chunk
+    d_win = torch.empty((R, W_t, REQ_BYTES), dtype=torch.uint8, device=dev)
+    for k in range(steps):
+        d_win[:, k * args.chunk:(k + 1) * args.chunk, :] = next_chunk().view(R, args.chunk, REQ_BYTES)
+    gen.close()
+    d_win_delay = torch.zeros(R * W_t, dtype=torch.int32, device=dev)
+    win_off = np.arange(R + 1, dtype=np.uint64) * np.uint64(W_t)
+    d_win_off = torch.from_numpy(win_off.view(np.int64)).to(dev)
+    d_pos = torch.from_numpy(win_off[:-1].copy().view(np.int64)).to(dev)
+    step_offs = [torch.from_numpy(np.concatenate([[0], win_off[:-1] + np.uint64((k + 1) * args.chunk)])
+                                  .astype(np.uint64).view(np.int64)).to(dev) for k in range(steps)]
+    torch.cuda.synchronize(dev)
+    log(f"[bench] timed requests resident: {R} x {W_t} in {time.time() - t_gen:.1f}s")
+    before = sum_stats(um, R)
+    per_before = [um.stats(r).as_dict() for r in range(R)] if os.environ.get("PU_PROF_RESET_AFTER_WARMUP") else None
+
+    # HIP events on the engine's (non-null) stream time exactly its launches
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        ev[k][0].record(stream)
+        if args.slice_ms > 0:
+            um.run_device_sliced(d_win.data_ptr(), d_win_off.data_ptr(), d_win_delay.data_ptr(), d_pos.data_ptr(),
+                                 int(args.slice_ms * 1000), sptr)
+        else:
+            um.run_device_sliced(d_win.data_ptr(), step_offs[k].data_ptr(), d_win_delay.data_ptr(), d_pos.data_ptr(),
+                                 0, sptr)
+        ev[k][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    log(f"[bench] timed {steps} steps in {elapsed:.3f}s; per-launch ms {['%.1f' % x for x in kern_ms]}")
+    pos = d_pos.cpu().numpy().view(np.uint64)
+    adv = (pos - win_off[:-1]).astype(np.int64)
+    log(f"[bench] requests per replica in the timed window: min {adv.min()} median {int(np.median(adv))} "
+        f"max {adv.max()} of {W_t}; {int((adv >= W_t).sum())} at the end (halted replicas skip to it)")
+    if keep_rep0:
+        rep0.append(d_win_delay[:int(adv[0])].cpu().numpy())
+    after = sum_stats(um, R)
+    per_replica = None
+    if per_before is not None:
+        per_after = [um.stats(r).as_dict() for r in range(R)]
+        keys = ("requests", "net_accesses", "net_distance", "mg1_calls", "lockdown_calls", "dram_accesses",
+                "total_num_broadcast", "L0_miss", "directory_ins", "directory_miss", "net_total_delay")
+        per_replica = {k: [int(per_after[r][k] - per_before[r][k]) for r in range(R)] for k in keys}
+    delta = {k: after[k] - before.get(k, 0) for k in after if k != "error_flags"}
+    flags = um.error_flags(R)
+    halted = int(((flags & A.PU_ERRF_NEG_DELAY) != 0).sum())
+    del d_win, d_win_delay
+    return Pass(elapsed=elapsed, kern_ms=kern_ms, adv=adv, rep0=rep0, delta=delta, halted=halted,
+                errf=int(np.bitwise_or.reduce(flags)) if len(flags) else 0, per_replica=per_replica,
+                steps=steps, processed=int(delta["requests"]))
+
+
+def single_instance(cfg, args, dev, threads) -> dict:
+    """ONE simulation alone on the GPU: replica 0's stream, the same warmup,
+    then --single-requests requests in one launch (HIP events)."""
+    import torch
+
+    import primesim_amd as P
+    from primesim_amd.dist import replica_seed
+    n_w, n_t = args.warmup * args.chunk, args.single_requests
+    reqs = P.generate_stream(stream_spec(replica_seed(SEED_BASE, 0, 0), n_w + n_t))
+    um = P.UncoreManager()
+    um.init(cfg, replicas=1, device=dev.index)
+    for prog, th in threads:
+        um.allocCore(prog, th)
+    stream = torch.cuda.Stream(dev)
+    d_req = torch.from_numpy(reqs.view(np.uint8)).to(dev)
+    d_delay = torch.zeros(len(reqs), dtype=torch.int32, device=dev)
+    off_w = torch.tensor([0, n_w], dtype=torch.int64, device=dev)
+    off_t = torch.tensor([0, n_w + n_t], dtype=torch.int64, device=dev)
+    pos = torch.tensor([n_w], dtype=torch.int64, device=dev)
+    um.run_device(d_req.data_ptr(), off_w.data_ptr(), d_delay.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    um.run_device_sliced(d_req.data_ptr(), off_t.data_ptr(), d_delay.data_ptr(), pos.data_ptr(), 0, stream.cuda_stream)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1)
+    st = um.stats(0).as_dict()
+    um.close()
+    return {"value": n_t / (ms / 1e3), "unit": "accesses/s", "requests": n_t, "kernel_ms": ms, "wall_s": wall,
+            "sample": f"one C4 simulation alone on the GPU (replica 0's stream): {n_w} warmup requests, then "
+                      f"{n_t} requests in one launch; link visits/access {st['net_distance'] / st['requests']:.1f}",
+            "note": "one uncore is a sequential fold (one wavefront); DESIGN.md §8 measures how little of it a "
+                    "relaxation can parallelise"}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10, help="timed steps (default: the stream's second quantum)")
-    ap.add_argument("--warmup", type=int, default=10, help="untimed steps (default: the first quantum)")
+    ap.add_argument("--steps", type=int, default=10, help="timed steps")
+    ap.add_argument("--warmup", type=int, default=10, help="untimed steps of --chunk requests per replica")
     ap.add_argument("--replicas", type=int, default=0, help="replicas per GPU (0 = size to HBM)")
     ap.add_argument("--chunk", type=int, default=40960, help="requests per replica per step")
     ap.add_argument("--slice-ms", type=float, default=400.0,
                     help="timed steps are wall-time slices: every replica continues its own stream for this long "
                          "per launch (stopping only between requests); 0 = fixed --chunk requests per replica per step")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--ensemble-seconds", type=float, default=3.0)
+    ap.add_argument("--ensemble-workers", type=int, default=0, help="0 = every host core of this job's share")
+    ap.add_argument("--closed-steps", type=int, default=5, help="timed steps of the closed-loop pass (0 = skip)")
+    ap.add_argument("--single-requests", type=int, default=40960)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="headline only (profiling runs)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) normally; gloo for CPU-side rehearsal")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC traffic summary written by tools/pmc_traffic.py for this kernel")
+                    help="PMC traffic summary written by tools/pmc_traffic.py for this build")
     args = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    extras = rank == 0 and world == 1 and not args.no_extras
 
     import primesim_amd as P
     from primesim_amd import _abi as A
     from primesim_amd import config as CF
     from primesim_amd.dist import reduce_run, replica_seed
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    sim = CF.preset("C4")
+    xml_path = os.path.join(tempfile.gettempdir(), f"pu_bench_c4_{os.getpid()}.xml")
+    CF.write_xml(sim, xml_path)
+    cfg = P.load_config(xml_path)
+    threads = P.stream_threads(stream_spec(SEED_BASE))
+
+    # ---- the CPU ensemble forks now, before this process touches the GPU
+    ens = None
+    if extras and not args.no_cpu:
+        nw = args.ensemble_workers or host_core_share()
+        ens = Ensemble(xml_path, nw, args.warmup * args.chunk, args.steps * args.chunk, args.ensemble_seconds)
+
+    import torch
+    import torch.distributed as dist
     if world > 1:
         dist.init_process_group(args.dist_backend, init_method="env://")
     # PU_BENCH_DEVICE pins every rank to one card (rehearsing N>1 on a 1-GPU box)
@@ -142,13 +416,7 @@ def main() -> None:
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    sim = CF.preset("C4")
-    xml_path = os.path.join(tempfile.gettempdir(), f"pu_bench_c4_{os.getpid()}.xml")
-    CF.write_xml(sim, xml_path)
-    cfg = P.load_config(xml_path)
-
     # ---- per-replica HBM: engine state + the timed request slabs + one warmup chunk
-    um = P.UncoreManager()
     probe = P.UncoreManager()
     probe.init(cfg, replicas=1, device=local)
     rbytes = probe.replica_bytes
@@ -162,148 +430,95 @@ def main() -> None:
     R = max(1, R - R % 8) if R >= 8 else R
     log(f"[bench] rank {rank}: replica {rbytes / 2**20:.0f} MiB + requests {(per_bytes - rbytes) / 2**20:.0f} MiB, "
         f"{R} replicas (resident limit {resident}), free {free / 2**30:.0f} GiB")
-    global LAST_REPLICAS
+    global LAST_REPLICAS, LAST_PER_REPLICA
     LAST_REPLICAS = R
+    um = P.UncoreManager()
     um.init(cfg, replicas=R, device=local)
-    threads = P.stream_threads(P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024))
     for prog, th in threads:
         um.allocCore(prog, th)
-
-    # ---- request streams: one seed per replica (disjoint across ranks), produced
-    # chunk by chunk in canonical order by the resumable host generator
-    specs = [P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=replica_seed(4, rank, r), num_quanta=64)
-             for r in range(R)]
-    gen = P.StreamSet(specs)
-    host = np.zeros((R, args.chunk), dtype=A.REQ_DTYPE)
-    offs = torch.from_numpy((np.arange(R + 1, dtype=np.uint64) * np.uint64(args.chunk)).view(np.int64)).to(dev)
-    # a dedicated (non-null) stream: the engine launches on it and the HIP
-    # events below time exactly those launches
     stream = torch.cuda.Stream(dev)
-    sptr = stream.cuda_stream
-    assert sptr != 0
-    rep0 = []                                       # replica 0's delays, for the parity check
+    assert stream.cuda_stream != 0
 
-    def next_chunk() -> torch.Tensor:
-        got = gen.next_into(host)
-        assert got == args.chunk, (got, args.chunk)
-        return torch.from_numpy(host.view(np.uint8).reshape(-1)).to(dev)
-
-    # warmup: the first quantum of every replica's stream (all 1024 cores, cold
-    # caches, empty link histories); untimed, requests uploaded step by step
-    d_warm_delay = torch.zeros(R * args.chunk, dtype=torch.int32, device=dev)
-    t_w = time.time()
-    for s in range(args.warmup):
-        d_req = next_chunk()
-        um.run_device(d_req.data_ptr(), offs.data_ptr(), d_warm_delay.data_ptr(), sptr)
-        torch.cuda.synchronize(dev)
-        rep0.append(d_warm_delay[:args.chunk].cpu().numpy())
-        del d_req
-        log(f"[bench] warmup step {s} done ({time.time() - t_w:.1f}s)")
-    if os.environ.get("PU_PROF_RESET_AFTER_WARMUP"):   # tools/prof_regions.py: count the timed steps only
-        P.uncore.lib().pu_engine_prof_read(None, 0, 1)
-    # timed window: the next steps x chunk requests of every replica, generated
-    # and made resident in HBM first, replica-major ([R][steps*chunk])
-    t_gen = time.time()
-    W_t = args.steps * args.chunk
-    d_win = torch.empty((R, W_t, REQ_BYTES), dtype=torch.uint8, device=dev)
-    for k in range(args.steps):
-        d_win[:, k * args.chunk:(k + 1) * args.chunk, :] = next_chunk().view(R, args.chunk, REQ_BYTES)
-    d_win_delay = torch.zeros(R * W_t, dtype=torch.int32, device=dev)
-    win_off = np.arange(R + 1, dtype=np.uint64) * np.uint64(W_t)
-    d_win_off = torch.from_numpy(win_off.view(np.int64)).to(dev)
-    d_pos = torch.from_numpy(win_off[:-1].copy().view(np.int64)).to(dev)
-    # fixed-size steps (--slice-ms 0): launch k covers [k*chunk, (k+1)*chunk) of every replica
-    step_offs = [torch.from_numpy(np.concatenate([[0], win_off[:-1] + np.uint64((k + 1) * args.chunk)])
-                                  .astype(np.uint64).view(np.int64)).to(dev) for k in range(args.steps)]
-    torch.cuda.synchronize(dev)
-    log(f"[bench] timed requests resident: {R} x {W_t} in {time.time() - t_gen:.1f}s")
-    before = sum_stats(um, R)
-    prof_keys = ("requests", "net_accesses", "net_distance", "mg1_calls", "lockdown_calls", "dram_accesses",
-                 "total_num_broadcast", "L0_miss", "directory_ins", "directory_miss", "net_total_delay")
-    per_before = None
-    if os.environ.get("PU_PROF_RESET_AFTER_WARMUP"):
-        per_before = [um.stats(r).as_dict() for r in range(R)]
-
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        if args.slice_ms > 0:
-            ev[k][0].record(stream)
-            um.run_device_sliced(d_win.data_ptr(), d_win_off.data_ptr(), d_win_delay.data_ptr(), d_pos.data_ptr(),
-                                 int(args.slice_ms * 1000), sptr)
-            ev[k][1].record(stream)
-        else:
-            ev[k][0].record(stream)
-            um.run_device_sliced(d_win.data_ptr(), step_offs[k].data_ptr(), d_win_delay.data_ptr(), d_pos.data_ptr(),
-                                 0, sptr)
-            ev[k][1].record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    log(f"[bench] timed {args.steps} steps in {elapsed:.3f}s; per-launch ms {['%.1f' % x for x in kern_ms]}")
-    pos = d_pos.cpu().numpy().view(np.uint64)
-    adv = (pos - win_off[:-1]).astype(np.int64)
-    log(f"[bench] requests per replica in the timed window: min {adv.min()} median {int(np.median(adv))} "
-        f"max {adv.max()} of {W_t}; {int((adv >= W_t).sum())} at the end (halted replicas skip to it)")
-    rep0.append(d_win_delay[:int(adv[0])].cpu().numpy())
-    gen.close()
-
-    after = sum_stats(um, R)
-    if per_before is not None:
-        global LAST_PER_REPLICA
-        per_after = [um.stats(r).as_dict() for r in range(R)]
-        LAST_PER_REPLICA = {k: [int(per_after[r][k] - per_before[r][k]) for r in range(R)] for k in prof_keys}
-    delta = {k: after[k] - before.get(k, 0) for k in after if k != "error_flags"}
-    errf = after.get("error_flags", 0)
-    # requests that actually reached the uncore: a replica whose message delay
-    # went negative stops there, like the reference's handler (prime.cpp:130-134)
-    processed = int(delta["requests"])
-    halted = sum(1 for r in range(R) if um.stats(r).error_flags & A.PU_ERRF_NEG_DELAY)
-    t_max, tot_processed = reduce_run(elapsed, processed, dev if args.dist_backend == "nccl" else None)
+    # ---- headline: open-loop replay
+    H = run_pass(um, args, R, rank, world, dev, stream, P.uncore.PU_REPLAY_OPEN, args.steps, keep_rep0=rank == 0)
+    LAST_PER_REPLICA = H.per_replica
+    t_max, tot_processed = reduce_run(H.elapsed, H.processed, dev if args.dist_backend == "nccl" else None)
     value = tot_processed / t_max
-
-    # ---- roofline of the engine kernel (per launch, this rank)
-    avg_ms = float(np.mean(kern_ms))
-    bytes_per_launch = alg_bytes(delta, cfg) / args.steps
+    avg_ms = float(np.mean(H.kern_ms))
+    bytes_per_launch = alg_bytes(H.delta, cfg) / args.steps
     achieved = bytes_per_launch / (avg_ms / 1e3) / 1e9
 
-    # HBM traffic from the PMC counters (FETCH_SIZE + WRITE_SIZE, separate rocprofv3
-    # passes of this same command, tools/pmc_traffic.py): bytes per access x this
-    # launch's accesses
-    traffic, traffic_src = None, None
-    if os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        traffic = tj["hbm_bytes_per_access"] * (processed / args.steps)
-        traffic_src = (f"{os.path.relpath(args.traffic_json, ROOT)}: {tj['hbm_bytes_per_access']:.0f} B/access "
-                       f"measured at {tj['replicas']} replicas x {tj['requests_per_replica_per_launch']} requests")
-
+    parity_ok = True
     result = None
     if rank == 0:
+        ens_res = ens.run() if ens is not None else None
+        if ens_res:
+            log(f"[bench] cpu ensemble ({ens_res['kind']}, {ens_res['cores']} processes): "
+                f"{ens_res['value']:.0f} accesses/s")
+        closed = None
+        if extras and args.closed_steps > 0:
+            um.reset()
+            C = run_pass(um, args, R, rank, world, dev, stream, P.uncore.PU_REPLAY_CLOSED, args.closed_steps,
+                         keep_rep0=True)
+            c_par = None
+            if not args.no_cpu:
+                import oracle as O
+                w0, n_t = args.warmup * args.chunk, args.closed_steps * args.chunk
+                s0 = P.generate_stream(stream_spec(replica_seed(SEED_BASE, 0, 0), w0 + n_t))
+                kind, n_cpu, el, d_cpu = cpu_baseline(xml_path, cfg, s0, threads, w0, 5.0, O.MODE_CLOSED)
+                gd = np.concatenate(C.rep0)
+                m = min(len(d_cpu), len(gd))
+                c_par = {"kind": kind, "requests_compared": m, "bit_identical": bool(np.array_equal(gd[:m], d_cpu[:m]))}
+                parity_ok &= c_par["bit_identical"]
+            closed = {"value": C.processed / C.elapsed, "unit": "accesses/s", "steps": C.steps,
+                      "per_simulation_accesses_per_s": C.processed / C.elapsed / R,
+                      "halted_replicas": C.halted,
+                      "mg1_share_of_link_visits": C.delta["mg1_calls"] / max(1, C.delta["net_distance"]),
+                      "mean_delay_cycles": 0.0,
+                      "parity": c_par}
+            gd = np.concatenate(C.rep0)
+            closed["mean_delay_cycles"] = float(gd[gd != 0].mean()) if (gd != 0).any() else 0.0
+            log(f"[bench] closed loop: {closed['value']:.4g} accesses/s, halted {C.halted}, "
+                f"M/G/1 share {closed['mg1_share_of_link_visits']:.3f}")
+        um.close()
+        single = single_instance(cfg, args, dev, threads) if extras else None
+        if single:
+            log(f"[bench] single instance: {single['value']:.0f} accesses/s")
         cpu = None
         if not args.no_cpu:
-            # replica 0's stream: the reference fills the warmup quantum untimed,
-            # then is timed on the requests of the GPU's timed window (as many as
-            # fit in --cpu-seconds); parity is checked on every request both ran
+            # replica 0's stream: the reference fills the warmup untimed, then is
+            # timed on the requests of the GPU's timed window (as many as fit in
+            # --cpu-seconds); parity is checked on every request both ran
             w0, n_t = args.warmup * args.chunk, args.steps * args.chunk
-            s0 = P.generate_stream(P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=replica_seed(4, rank, 0),
-                                                num_quanta=64, max_requests=w0 + n_t))
+            s0 = P.generate_stream(stream_spec(replica_seed(SEED_BASE, rank, 0), w0 + n_t))
             kind, n_cpu, el, d_cpu = cpu_baseline(xml_path, cfg, s0, threads, w0, args.cpu_seconds)
-            gpu_d = np.concatenate(rep0)
+            gpu_d = np.concatenate(H.rep0)
             m = min(len(d_cpu), len(gpu_d))
             parity = bool(np.array_equal(gpu_d[:m], d_cpu[:m]))
-            cpu = {"value": n_cpu / el, "unit": "accesses/s", "cores": 1, "kind": kind,
+            parity_ok &= parity
+            cpu = {"value": n_cpu / el, "unit": "accesses/s", "cores": 1, "kind": kind, "cpu_model": cpu_model(),
                    "sample": f"replica 0's C4 stream: requests {w0}..{w0 + n_cpu} (the GPU's timed window; the GPU "
-                             f"ran {int(adv[0])} of them for replica 0), after an untimed fill of the {w0}-request "
+                             f"ran {int(H.adv[0])} of them for replica 0), after an untimed fill of the {w0}-request "
                              f"warmup, single-threaded "
                              f"({'reference uncore compiled from /root/reference/src' if kind == 'reference' else 'oracle/cpu_ref restatement'}), "
-                             f"{el:.1f} s; GPU delays bit-identical on all {m} requests compared: {parity}"}
+                             f"{el:.1f} s; GPU delays bit-identical on all {m} requests compared: {parity}",
+                   "parity": parity}
             log(f"[bench] cpu baseline ({kind}): {n_cpu / el:.0f} accesses/s; parity on {m} delays: {parity}")
+
+        # fabric traffic measured by tools/pmc_traffic.py for this build only
+        traffic, traffic_src = None, None
+        if os.path.exists(args.traffic_json):
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            built = P.uncore.library_source_hash()
+            if tj.get("src_hash") == built:
+                traffic = tj["fabric_bytes_per_access"] * (H.processed / args.steps)
+                traffic_src = (f"{os.path.relpath(args.traffic_json, ROOT)}: {tj['fabric_bytes_per_access']:.0f} B/access "
+                               f"(FETCH_SIZE+WRITE_SIZE, separate PMC passes; fabric bytes incl. MALL hits) measured "
+                               f"on build {built} at {tj['replicas']} replicas")
+            else:
+                traffic_src = (f"not reported: {os.path.relpath(args.traffic_json, ROOT)} was measured on build "
+                               f"{tj.get('src_hash')}, this library is {built}")
         result = {
             "metric": METRIC,
             "value": value,
@@ -319,18 +534,22 @@ def main() -> None:
             "data": "synthetic",
             "config": {
                 "workload": "C4: 1024-core 32x32 mesh, L1 32KB/8W + 256KB/8W shared-LLC slice per tile, "
-                            "directory MESI full-map, uniform 2^20 lines + 64-line hotspot, 25% writes",
+                            "directory MESI full-map, uniform 2^20 lines + 64-line hotspot, 25% writes, open-loop replay",
                 "replicas_per_gpu": R,
                 "step": (f"wall-time slice: every replica continues its own stream for {args.slice_ms:g} ms per "
                          f"launch, stopping only between requests" if args.slice_ms > 0 else
                          f"fixed: {args.chunk} requests per replica per launch"),
-                "mean_requests_per_replica_per_step": processed / (R * args.steps),
+                "mean_requests_per_replica_per_step": H.processed / (R * args.steps),
                 "warmup_requests_per_replica": args.warmup * args.chunk,
                 "parallelism": f"replicas: {R} independent uncores per GPU x {world} GPU(s)",
-                "per_replica_accesses_per_s": value / (R * world),
-                "halted_replicas": halted,
-                "error_flags": errf & ~A.PU_ERRF_NEG_DELAY,
+                "halted_replicas": H.halted,
+                "mg1_share_of_link_visits": H.delta["mg1_calls"] / max(1, H.delta["net_distance"]),
+                "error_flags": H.errf & ~A.PU_ERRF_NEG_DELAY,
+                "engine_build": P.uncore.library_source_hash(),
             },
+            "per_simulation_accesses_per_s": value / (R * world),
+            "single_instance": single,
+            "closed_loop": closed,
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
@@ -339,20 +558,27 @@ def main() -> None:
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": "uncore_kernel<1, true>" if args.slice_ms > 0 else "uncore_kernel<1, true> (no budget)",
+                "kernel": "uncore_kernel<1, true>",
                 "avg_launch_ms": avg_ms,
                 "alg_bytes_per_launch": bytes_per_launch,
+                "limiter": "instruction issue and dependent-load latency (profiles/r2_*sq*), not HBM bandwidth",
             },
             "cpu_baseline": cpu,
+            "cpu_baseline_ensemble": ens_res,
+            "parity": parity_ok if not args.no_cpu else None,
         }
         print(json.dumps(result), flush=True)
-    um.close()
+    else:
+        um.close()
     try:
         os.remove(xml_path)
     except OSError:
         pass
     if world > 1:
         dist.destroy_process_group()
+    if not parity_ok:
+        log("[bench] PARITY FAILURE: GPU delays differ from the reference")
+        sys.exit(1)
 
 
 if __name__ == "__main__":

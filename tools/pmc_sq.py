@@ -6,7 +6,7 @@ instruction mixes and L2 hit/miss — each pass a separate rocprofv3 run of
 bench.py (counter-block limits: MI355X_MICROARCH.md; no --pmc pass is combined
 with a trace domain).  Sums over the timed launches (the last `steps`).
 
-    python tools/pmc_sq.py --out gpurun_out/sq.json -- --steps 3 --warmup 10 --no-cpu
+    python tools/pmc_sq.py --out gpurun_out/sq.json -- --steps 3 --warmup 5 --no-cpu --no-extras
 """
 from __future__ import annotations
 
@@ -26,6 +26,8 @@ PASSES = [
     ["SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_LDS", "SQ_INSTS_VALU",
      "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"],
     ["TCC_HIT_sum", "TCC_MISS_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_WRREQ_sum"],
+    ["SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_INSTS_LDS"],
+    ["SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU"],
 ]
 
 
@@ -65,6 +67,14 @@ def main() -> None:
             ids = sorted(per)[-steps:]
             out["per_launch"][name] = sum(per[k] for k in ids) / len(ids)
     pl = out["per_launch"]
+    if pl.get("SQ_LDS_IDX_ACTIVE"):
+        out["lds_bank_conflict_share"] = pl.get("SQ_LDS_BANK_CONFLICT", 0.0) / pl["SQ_LDS_IDX_ACTIVE"]
+    if pl.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in pl:
+        # rocprof's VALUUtilization: active lanes per VALU issue cycle / 64
+        out["valu_lane_utilization"] = pl["SQ_THREAD_CYCLES_VALU"] / (pl["SQ_ACTIVE_INST_VALU"] * 64.0)
+    sys.path.insert(0, ROOT)
+    from primesim_amd import uncore
+    out["src_hash"] = uncore.library_source_hash()
     if "SQ_WAVE_CYCLES" in pl and pl["SQ_WAVE_CYCLES"]:
         wc = pl["SQ_WAVE_CYCLES"]
         out["share_of_wave_cycles"] = {k: pl[k] / wc for k in pl if k.startswith(("SQ_WAIT", "SQ_ACTIVE"))}

@@ -10,7 +10,10 @@ streaming reads; this kernel's reads are 8-40 B per lane gathers, for which the
 guide gives no calibration, so the raw figure is reported next to a 2x-read
 upper bound and both are labelled.
 
-    python tools/pmc_traffic.py --out profiles/r1_traffic.json -- --steps 3 --warmup 1 --no-cpu
+    python tools/pmc_traffic.py --out profiles/traffic.json -- --steps 5 --warmup 5 --no-cpu --no-extras
+
+The summary carries the library's source hash (pu_version): bench.py reports
+`roofline.traffic` only from a summary measured on the build it runs.
 
 Writes the summary JSON, and copies the rocprofv3 summaries under profiles/.
 """
@@ -87,23 +90,29 @@ def main():
     accesses = R * chunk
     raw = (f_kb + w_kb) * 1024.0
     upper = (2.0 * f_kb + w_kb) * 1024.0
+    sys.path.insert(0, ROOT)
+    from primesim_amd import uncore
     out = {
         "kernel": KERNEL,
+        "src_hash": uncore.library_source_hash(),
         "launches_measured": steps,
         "warmup": warm,
         "replicas": R,
         "requests_per_replica_per_launch": chunk,
         "fetch_size_kb_per_launch": f_kb,
         "write_size_kb_per_launch": w_kb,
-        "hbm_bytes_per_launch": raw,
-        "hbm_bytes_per_launch_read_x2_bound": upper,
-        "hbm_bytes_per_access": raw / accesses,
+        "fabric_bytes_per_launch": raw,
+        "fabric_bytes_per_launch_read_x2_bound": upper,
+        "fabric_bytes_per_access": raw / accesses,
+        "fabric_read_bytes_per_access": f_kb * 1024.0 / accesses,
+        "fabric_write_bytes_per_access": w_kb * 1024.0 / accesses,
         "alg_bytes_per_launch": bench_line["roofline"]["alg_bytes_per_launch"],
         "alg_bytes_per_access": bench_line["roofline"]["alg_bytes_per_launch"] / accesses,
         "avg_launch_ms_under_profiler": bench_line["roofline"]["avg_launch_ms"],
-        "note": "FETCH_SIZE+WRITE_SIZE (KB) x 1024 per timed launch, separate --pmc passes; gfx950 halves "
-                "FETCH_SIZE for 16-B/lane streaming reads (MI355X_MICROARCH.md §HBM), uncalibrated for this "
-                "kernel's 8-40 B gathers, hence the x2-read bound",
+        "note": "FETCH_SIZE+WRITE_SIZE (KB) x 1024 per timed launch, separate --pmc passes. These are the L2's "
+                "memory-side (fabric) requests: Infinity-Cache hits are counted, so this is fabric traffic, an "
+                "upper bound on HBM bytes. gfx950 halves FETCH_SIZE for 16-B/lane streaming reads "
+                "(MI355X_MICROARCH.md §HBM), uncalibrated for this kernel's 8-40 B gathers, hence the x2-read bound",
         "bench_args": bargs,
     }
     with open(a.out, "w") as f:
