@@ -121,6 +121,17 @@ enum StatId {
 };
 static __shared__ unsigned long long lds_stat[SN_COUNT];
 static __shared__ unsigned long long lds_err;
+// The message loop's state (uncore_kernel), lane 0 its writer.
+struct LoopCtl {
+    int64_t msg_shift;     // PU_KF_CLOSED: core shift at the open message's start
+    uint64_t dead_tags;    // PU_KF_MSGHALT: receive threads that have exited
+    uint64_t deadline;     // s_memrealtime at which a time-sliced launch stops
+    uint64_t done;         // requests processed in this launch
+    int32_t D;             // prime.cpp's running `delay` of the open message
+    int32_t halted, halted0, skip;
+    uint32_t flags, _pad;
+};
+static __shared__ LoopCtl lds_ctl;
 
 __device__ __forceinline__ void stat_add(int k, uint64_t v) {
     if (lane_id() == 0) atomicAdd(&lds_stat[k], (unsigned long long)v);
@@ -1703,78 +1714,90 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PU_MIN_WAVES
     const uint64_t blk_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
 
+    // The message loop's own state lives in LDS (lane 0 writes, every lane reads
+    // it back wave-uniform): nothing of it stays in registers across the
+    // inlined access(), whose register budget is tight (4 waves/SIMD).
     RunState* rs = e.template at<RunState>(g->off_run);
-    int32_t D = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->batch_delay : 0u, 0);
-    const int32_t halted0 = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->halted : 0u, 0);
-    const bool keep_halt = (flags & PU_KF_NOHALT) == 0;
-    int32_t halted = keep_halt ? halted0 : 0;
-    int32_t skip_msg = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->skip_msg : 0u, 0);
-    int64_t msg_shift = (int64_t)rl64(e.ln == 0 ? (uint64_t)rs->msg_shift : 0ull, 0);
-    uint64_t dead_tags = rl64(e.ln == 0 ? rs->dead_tags : 0ull, 0);
-    int64_t* core_shift = e.template at<int64_t>(g->off_core_shift);
+    if (e.ln == 0) {
+        const int32_t h0 = rs->halted;
+        lds_ctl.D = rs->batch_delay;
+        lds_ctl.halted0 = h0;
+        lds_ctl.halted = (flags & PU_KF_NOHALT) ? 0 : h0;
+        lds_ctl.skip = rs->skip_msg;
+        lds_ctl.flags = flags;
+        lds_ctl.msg_shift = rs->msg_shift;
+        lds_ctl.dead_tags = rs->dead_tags;
+        lds_ctl.deadline = budget_ticks ? wave_t0 + budget_ticks : UINT64_MAX;
+        lds_ctl.done = 0;
+    }
+    __builtin_amdgcn_wave_barrier();
     e.pool_top = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->pool_top : 0u, 0);
     e.page_next = rl64(e.ln == 0 ? rs->page_next : 0ull, 0);
     e.last_addr = rl64(e.ln == 0 ? rs->last_addr : 0ull, 0);
     e.stop = false;
-    int64_t* completion = e.template at<int64_t>(g->off_completion);
     const uint64_t b = pos ? pos[blockIdx.x] : off[blockIdx.x], end = off[blockIdx.x + 1];
-    uint64_t done = 0;
     uint64_t i = b;
     for (; i < end; i++) {
-        if (budget_ticks && __builtin_amdgcn_s_memrealtime() - wave_t0 >= budget_ticks) break;
-        if (halted) {                       // the reference's handler thread has exited
+        if (SLICED && __builtin_amdgcn_s_memrealtime() >= uni64(lds_ctl.deadline)) break;
+        if (uni32((uint32_t)lds_ctl.halted)) {   // the reference's handler thread has exited
             if (e.ln == 0) delays[i] = 0;
             continue;
         }
         PROF_T(p_loop);
         const pu_req q = reqs[i];
         const bool core_ok = q.core >= 0 && q.core < g->num_cores;
-        if (q.batch_start) {
-            D = 0;
-            skip_msg = (flags & PU_KF_MSGHALT) ? (int32_t)((dead_tags >> (q.tag & 63)) & 1) : 0;
-            if ((flags & PU_KF_CLOSED) && core_ok)
-                msg_shift = (int64_t)rl64(e.ln == 0 ? (uint64_t)core_shift[q.core] : 0ull, 0);
+        const uint32_t fl = uni32(lds_ctl.flags);
+        if (q.batch_start && e.ln == 0) {
+            lds_ctl.D = 0;
+            lds_ctl.skip = (fl & PU_KF_MSGHALT) ? (int32_t)((lds_ctl.dead_tags >> (q.tag & 63)) & 1) : 0;
+            if ((fl & PU_KF_CLOSED) && core_ok)
+                lds_ctl.msg_shift = e.template at<int64_t>(g->off_core_shift)[q.core];
         }
-        if (skip_msg) {                     // PU_KF_MSGHALT: this message's handler thread has exited
+        __builtin_amdgcn_wave_barrier();
+        if (uni32((uint32_t)lds_ctl.skip)) {     // PU_KF_MSGHALT: this message's receive thread has exited
             if (e.ln == 0) delays[i] = 0;
             continue;
         }
         PROF_ADD(PF_REQ, p_loop);
-        const int64_t t = q.timer + ((flags & PU_KF_CLOSED) ? msg_shift : 0) + D;
+        const int64_t shift = (fl & PU_KF_CLOSED) ? (int64_t)uni64((uint64_t)lds_ctl.msg_shift) : 0;
+        const int64_t t = q.timer + shift + (int32_t)uni32((uint32_t)lds_ctl.D);
         Req r{q.addr, q.prog_id, (int32_t)q.mem_type};
         int d = e.access(q.core, r, t);
-        D += d - 1;
         if (e.ln == 0) {
+            const int32_t D = lds_ctl.D + d - 1;
+            lds_ctl.D = D;
+            lds_ctl.done++;
             delays[i] = d;
             if (core_ok) {
-                completion[q.core] = t + d;
-                if (flags & PU_KF_CLOSED) core_shift[q.core] = msg_shift + D;
+                e.template at<int64_t>(g->off_completion)[q.core] = t + d;
+                if (lds_ctl.flags & PU_KF_CLOSED)
+                    e.template at<int64_t>(g->off_core_shift)[q.core] = lds_ctl.msg_shift + D;
+            }
+            if (D < 0) {                         // prime.cpp:130-134
+                err_or(PU_ERRF_NEG_DELAY);
+                if (lds_ctl.flags & PU_KF_MSGHALT) {
+                    lds_ctl.skip = 1;
+                    lds_ctl.dead_tags |= 1ull << (q.tag & 63);
+                } else if (!(lds_ctl.flags & PU_KF_NOHALT)) {
+                    lds_ctl.halted = 1;
+                }
+            }
+            if (e.stop) {                        // engine limit hit: cannot continue exactly
+                lds_ctl.halted = 1;
+                lds_ctl.skip = 0;
             }
         }
-        done++;
-        if (D < 0) {                        // prime.cpp:130-134
-            err_or(PU_ERRF_NEG_DELAY);
-            if (flags & PU_KF_MSGHALT) {
-                skip_msg = 1;
-                dead_tags |= 1ull << (q.tag & 63);
-            } else if (keep_halt) {
-                halted = 1;
-            }
-        }
-        if (e.stop) {                       // engine limit hit: cannot continue exactly
-            halted = 1;
-            skip_msg = 0;
-        }
+        __builtin_amdgcn_wave_barrier();
         PROF_ADD(PF_LOOP, p_loop);
     }
     if (e.ln == 0) {
         if (pos) pos[blockIdx.x] = i;
-        rs->batch_delay = D;
-        rs->halted = keep_halt ? halted : (halted0 | halted);
-        rs->skip_msg = skip_msg;
-        rs->msg_shift = msg_shift;
-        rs->dead_tags = dead_tags;
-        rs->processed += done;
+        rs->batch_delay = lds_ctl.D;
+        rs->halted = (lds_ctl.flags & PU_KF_NOHALT) ? (lds_ctl.halted0 | lds_ctl.halted) : lds_ctl.halted;
+        rs->skip_msg = lds_ctl.skip;
+        rs->msg_shift = lds_ctl.msg_shift;
+        rs->dead_tags = lds_ctl.dead_tags;
+        rs->processed += lds_ctl.done;
         rs->pool_top = e.pool_top;
         rs->page_next = e.page_next;
         rs->last_addr = e.last_addr;

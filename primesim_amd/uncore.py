@@ -40,6 +40,14 @@ def lib() -> C.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise UncoreError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    # One HIP runtime per process: PyTorch bundles its own libamdhip64 under the
+    # same SONAME (libamdhip64.so.7) but NEEDs it as "libamdhip64.so", so if this
+    # library loaded /opt/rocm's copy first, torch would load a second runtime
+    # and find no GPU.  Loading torch first makes both share torch's runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     P = C.POINTER
     sig = {
