@@ -177,8 +177,9 @@ typedef struct pu_stats {
                                              2 GiB of bitmaps; PRIMEUNCORE_POOL_ENTRIES) */
 #define PU_ERRF_PAGES        (1ull << 6)  /* page table 3/4 full (engine limit: 2^22 slots,
                                              raise PRIMEUNCORE_PAGE_ENTRIES) */
-#define PU_ERRF_PROG         (1ull << 7)  /* no longer raised (directory lines hold the
-                                             full int prog_id since 0.2) */
+#define PU_ERRF_PROG         (1ull << 7)  /* no longer raised: since 0.2 directory lines
+                                             carry any int prog_id (ids outside [0, 1023)
+                                             escape to a side array) */
 /* The bits that mean the replica stopped where the reference would have
  * continued (an engine limit) or reached a state the reference leaves undefined.
  * Not CORE_RANGE (System::access returns -1 and goes on) nor NEG_DELAY

@@ -992,11 +992,16 @@ struct Engine {
     // `sh`, ascending, 16 bits each (12 bits each in the stored DirLine word);
     // a fifth sharer moves the set to a full-map bitmap from the replica's pool
     // (lane k holds word k).
-    static __device__ __forceinline__ uint64_t dir_word(uint32_t nsh, uint64_t sh, uint32_t st) {
+    // the line's 10-bit program field: the id itself, or the escape for ids
+    // outside [0, 1023) (their full value goes to the side array)
+    static __device__ __forceinline__ uint32_t prog10(int prog) {
+        return (uint32_t)prog < PU_DIR_PROG_ESC ? (uint32_t)prog : PU_DIR_PROG_ESC;
+    }
+    static __device__ __forceinline__ uint64_t dir_word(uint32_t nsh, uint64_t sh, uint32_t st, uint32_t p10) {
         const uint64_t s = nsh == PU_SH_POOL ? sh
                          : (sh & 0xFFFull) | ((sh >> 4) & 0xFFF000ull) | ((sh >> 8) & 0xFFF000000ull) |
                            ((sh >> 12) & 0xFFF000000000ull);
-        return s | ((uint64_t)(nsh == PU_SH_POOL ? 7u : nsh) << 48) | ((uint64_t)st << 51);
+        return s | ((uint64_t)(nsh == PU_SH_POOL ? 7u : nsh) << 48) | ((uint64_t)st << 51) | ((uint64_t)p10 << 54);
     }
     static __device__ __forceinline__ uint32_t dir_state(uint64_t w) { return (uint32_t)(w >> 51) & 7u; }
     static __device__ __forceinline__ void dir_sharers(uint64_t w, uint32_t& nsh, uint64_t& sh) {
@@ -1170,10 +1175,18 @@ struct Engine {
         if (mine) {
             m = lines[line0 + (uint64_t)ln];
         } else {
-            m.tag = 0; m.ts = INT64_MAX; m.w = 0; m.prog = 0; m._pad = 0;
+            m.tag = 0; m.ts = INT64_MAX; m.w = 0;
         }
         const uint32_t m_state = dir_state(m.w);
-        const uint64_t hm = ballot(mine && m_state != ST_I && m.prog == r.prog && m.tag == tag);
+        // program ids: the 10-bit field decides unless either side is escaped;
+        // the side array is read only then (ids >= 1023 or negative)
+        const uint32_t want10 = prog10(r.prog), m_p10 = (uint32_t)(m.w >> 54);
+        int32_t* side = at<int32_t>(D.off_prog);
+        int32_t m_prog = (int32_t)m_p10;
+        if (want10 == PU_DIR_PROG_ESC || ballot(mine && m_p10 == PU_DIR_PROG_ESC)) {
+            if (mine && m_p10 == PU_DIR_PROG_ESC) m_prog = side[line0 + (uint64_t)ln];
+        }
+        const uint64_t hm = ballot(mine && m_state != ST_I && m_prog == r.prog && m.tag == tag);
         int way = hm ? (int)__builtin_ctzll(hm) : -1;
         PROF_ADD(PF_HOME_LD, p_ld);
         count(D.off_cnt, home, 0);
@@ -1203,7 +1216,7 @@ struct Engine {
             if (!inv) {
                 old_st = dir_state(ww);
                 old_addr = (set << D.offbits) | (rl64(m.tag, way) << (D.offbits + D.idxbits));
-                old_prog = (int)rl32((uint32_t)m.prog, way);
+                old_prog = (int)rl32((uint32_t)m_prog, way);
             }
             dir_sharers(ww, nsh, sh);
             if (old_st != ST_I) {
@@ -1289,7 +1302,8 @@ struct Engine {
         *out_state = st == ST_B ? ST_S : st;
         if (ln == way) {
             // home slices stamp the arrival time (Q4)
-            lines[line0 + (uint64_t)way] = DirLine{tag, timer, dir_word(nsh, sh, st), r.prog, 0u};
+            lines[line0 + (uint64_t)way] = DirLine{tag, timer, dir_word(nsh, sh, st, want10)};
+            if (want10 == PU_DIR_PROG_ESC) side[line0 + (uint64_t)way] = r.prog;
         }
         return delay;
     }

@@ -58,22 +58,22 @@ struct LineMeta {
 };
 
 // Directory / shared-LLC line (reference Line, cache.h:77-87, with sharer_set),
-// 32 B (two 16-B loads per way):
+// 24 B (measured: 32-B lines made the C4 bench 3.5% slower):
 //   w bits  0-47  sharers: up to 4 LLC ids ascending, 12 bits each (< 4096
 //                 nodes), or the pool index of a full-map bitmap
 //         bits 48-50  sharer count 0..4, 7 = pool
 //         bits 51-53  state
-//   prog  the program id (InsMem::prog_id, any int)
+//         bits 54-63  program id if 0 <= id < 1023; 1023 = escaped: the full int
+//                     id (InsMem::prog_id) is in the side array DirGeo.off_prog
 // The engine works on the unpacked form (16-bit inline ids, nsh PU_SH_POOL).
 struct DirLine {
     uint64_t tag;
     int64_t ts;
     uint64_t w;
-    int32_t prog;
-    uint32_t _pad;
 };
 #define PU_SH_INLINE 4
 #define PU_SH_POOL 0xFF
+#define PU_DIR_PROG_ESC 1023u
 
 struct QueueHdr {
     uint32_t head;
@@ -120,6 +120,7 @@ struct DirGeo {
     int32_t offbits, idxbits, access_time, nwords;
     int32_t pool_entries, cset_shift;
     uint64_t off_line, off_pool, off_pool_free, off_alive, off_cnt;
+    uint64_t off_prog;     // int32 per line: the full program id of escaped lines
 };
 
 // Per-core TLBs and the first-touch page table (reference system.cpp:897-918,

@@ -204,6 +204,7 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
     // directory block, from counters that stay 0)
     uint64_t dlines = bus_sys ? 0 : (uint64_t)N * D.csets * D.nways;
     D.off_line = lay.take(dlines * sizeof(DirLine));
+    D.off_prog = lay.take(dlines * sizeof(int32_t));
     // sharer sets of more than 4 LLCs live in pool bitmaps: one entry per
     // directory line (a line holds at most one, so the pool cannot run out)
     // unless that exceeds 2 GiB of bitmaps; then as many as fit, and running
