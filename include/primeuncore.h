@@ -289,6 +289,12 @@ long pu_report(pu_handle* h, int replica, int include_time, char* buf, size_t ca
  * measured with HIP events on the engine's stream. */
 double pu_last_kernel_ms(pu_handle* h);
 
+/* UncoreManager::getSimStartTime / getSimFinishTime (uncore_manager.cpp:52-60):
+ * wall-clock stamps (CLOCK_REALTIME); pu_report(include_time=1) prints their
+ * difference as "Total computation time" like UncoreManager::report (:92-93). */
+void pu_sim_start_time(pu_handle* h);
+void pu_sim_finish_time(pu_handle* h);
+
 const char* pu_last_error(void);
 const char* pu_version(void);
 

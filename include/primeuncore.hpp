@@ -18,6 +18,16 @@
 
 namespace pu {
 
+// prime.cpp:130-134: the message's running delay went negative at `index`;
+// the reference's handler thread prints an error and returns without a reply.
+struct NegativeDelay : std::runtime_error {
+    size_t index;
+    int delay;
+    NegativeDelay(size_t i, int d)
+        : std::runtime_error("negative delay at request " + std::to_string(i) + ": " + std::to_string(d)),
+          index(i), delay(d) {}
+};
+
 // The fields of the reference InsMem (cache.h:92-99) that System::access reads.
 struct InsMem {
     char mem_type;       // 0 read, 1 write
@@ -47,17 +57,29 @@ class UncoreManager {
         init(&cfg, replicas, device);
     }
 
+    // UncoreManager::getSimStartTime / getSimFinishTime (uncore_manager.cpp:52-60).
+    void getSimStartTime() { pu_sim_start_time(h_); }
+    void getSimFinishTime() { pu_sim_finish_time(h_); }
+
     int allocCore(int prog_id, int thread_id) { return pu_alloc_core(h_, prog_id, thread_id); }
     int deallocCore(int prog_id, int thread_id) { return pu_dealloc_core(h_, prog_id, thread_id); }
     int getCoreId(int prog_id, int thread_id) { return pu_get_core_id(h_, prog_id, thread_id); }
 
-    // UncoreManager::uncore_access (uncore_manager.cpp:82-85): -1 if core_id >= num_cores.
+    // UncoreManager::uncore_access (uncore_manager.cpp:82-85): -1 if core_id >=
+    // num_cores; a negative value when the reference's int wraps; throws on an
+    // engine error (PU_E* codes).
     int uncore_access(int core_id, InsMem* ins, int64_t timer) {
-        return pu_access(h_, core_id, ins->prog_id, ins->mem_type, &ins->addr_dmem, timer);
+        int d = pu_access(h_, core_id, ins->prog_id, ins->mem_type, &ins->addr_dmem, timer);
+        if (d == PU_EINVAL || d == PU_ENOMEM || d == PU_ENODEV || d == PU_ERANGE || d == PU_EIO ||
+            d == PU_ENOTSUP || d == PU_ESTATE)
+            throw std::runtime_error(pu_last_error());
+        return d;
     }
 
     // One MEM_REQUESTS message (prime.cpp:120-137): returns the `delay` prime.cpp
-    // sends back (sum of (d_i - 1)), or throws on engine errors.
+    // sends back (sum of (d_i - 1)).  Throws NegativeDelay where prime.cpp's
+    // handler would exit (the replica then stops, as that handler does), and
+    // runtime_error on engine errors (PU_ESTATE: an engine limit).
     int access_message(int core_id, int prog_id, const bool* mem_type, const uint64_t* addr,
                        const int64_t* timer, size_t n, int replica = 0) {
         static_assert(sizeof(bool) == sizeof(char), "MsgMem bool is one byte");
@@ -76,7 +98,10 @@ class UncoreManager {
         if (pu_access_batch(h_, replica, reqs_.data(), n, delays_.data()) != 0)
             throw std::runtime_error(pu_last_error());
         int delay = 0;
-        for (size_t i = 0; i < n; i++) delay += delays_[i] - 1;
+        for (size_t i = 0; i < n; i++) {
+            delay += delays_[i] - 1;
+            if (delay < 0) throw NegativeDelay(i, delay);   // later delays were never computed
+        }
         return delay;
     }
 

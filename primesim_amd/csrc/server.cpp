@@ -140,7 +140,7 @@ struct EngineExec : Exec {
     int32_t* d_delays = nullptr;
     uint64_t* d_off = nullptr;
     size_t cap = 0;
-    explicit EngineExec(pu_handle* hh) : h(hh), R(pu_num_replicas(hh)) {}
+    explicit EngineExec(pu_handle* hh) : h(hh), R(pu_num_replicas(hh)) { pu_sim_start_time(hh); }   // prime.cpp:207
     ~EngineExec() override {
         if (d_reqs) (void)hipFree(d_reqs);
         if (d_delays) (void)hipFree(d_delays);
@@ -184,6 +184,7 @@ struct EngineExec : Exec {
     int dealloc(int s, int p, int t) override { return pu_dealloc_core_replica(h, s, p, t); }
     int get(int s, int p, int t) override { return pu_get_core_id_replica(h, s, p, t); }
     std::string report(int s) override {
+        pu_sim_finish_time(h);                      // prime.cpp:232-233
         long len = pu_report(h, s, 1, nullptr, 0);
         if (len < 0) return std::string();
         std::string out((size_t)len + 1, '\0');

@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <ctime>
 #include <cstddef>
 #include <cstdlib>
 #include <cstdio>
@@ -253,6 +254,7 @@ struct pu_handle {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0.0;
+    struct timespec sim_start{}, sim_finish{};   // UncoreManager::sim_start_time / sim_finish_time
     uint32_t replay_flags = 0;   // PU_KF_CLOSED under PU_REPLAY_CLOSED
     // ThreadSched (thread_sched.cpp): the shared one, and per-replica copies
     // made on first use of a per-replica call (pu_*_core_replica: the server's
@@ -642,6 +644,13 @@ int pu_synchronize(pu_handle* h) {
 
 double pu_last_kernel_ms(pu_handle* h) { return h ? h->last_ms : 0.0; }
 
+void pu_sim_start_time(pu_handle* h) {
+    if (h) clock_gettime(CLOCK_REALTIME, &h->sim_start);
+}
+void pu_sim_finish_time(pu_handle* h) {
+    if (h) clock_gettime(CLOCK_REALTIME, &h->sim_finish);
+}
+
 int pu_core_completion(pu_handle* h, int replica, int64_t* out, size_t n) {
     if (!h || !out) return pu::set_error(PU_EINVAL, "bad arguments");
     if (replica < 0 || replica >= h->R) return pu::set_error(PU_ERANGE, "replica out of range");
@@ -721,7 +730,11 @@ long pu_report(pu_handle* h, int replica, int include_time, char* buf, size_t ca
     o << "*********************************************************\n";
     o << "*                   PriME Simulator                     *\n";
     o << "*********************************************************\n\n";
-    if (include_time) o << "Total computation time: " << h->last_ms / 1000.0 << " seconds\n";
+    if (include_time) {                  // uncore_manager.cpp:92-93
+        double sim_time = (double)(h->sim_finish.tv_sec - h->sim_start.tv_sec) +
+                          (double)(h->sim_finish.tv_nsec - h->sim_start.tv_nsec) / 1000000000.0;
+        o << "Total computation time: " << sim_time << " seconds\n";
+    }
     o << std::endl;
     o << "Core Allocation:\n";
     for (const auto& kv : h->sched_of(replica).map)

@@ -76,6 +76,8 @@ def lib() -> C.CDLL:
         "pu_last_error": (C.c_char_p, []),
         "pu_version": (C.c_char_p, []),
         "pu_set_replay_mode": (C.c_int, [C.c_void_p, C.c_int]),
+        "pu_sim_start_time": (None, [C.c_void_p]),
+        "pu_sim_finish_time": (None, [C.c_void_p]),
         "pu_error_flags": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
         "pu_stream_count": (C.c_int64, [P(A.StreamParams)]),
         "pu_stream_generate": (C.c_int64, [P(A.StreamParams), C.c_void_p, C.c_size_t]),
@@ -405,6 +407,13 @@ class UncoreManager:
         if rc != 0:
             raise UncoreError(f"access_batch: {last_error()}")
         return out
+
+    # UncoreManager::getSimStartTime / getSimFinishTime (uncore_manager.cpp:52-60)
+    def getSimStartTime(self) -> None:
+        lib().pu_sim_start_time(self._handle())
+
+    def getSimFinishTime(self) -> None:
+        lib().pu_sim_finish_time(self._handle())
 
     def set_replay_mode(self, mode: int) -> None:
         """PU_REPLAY_OPEN (recorded timers) or PU_REPLAY_CLOSED (timer_i += the
