@@ -99,7 +99,9 @@ struct QState {
 };
 
 #define AS1 __attribute__((address_space(1)))
+#ifndef PU_RING_PF
 #define PU_RING_PF 4   // staged rings in flight per wave (8 KB LDS)
+#endif
 // Waves per SIMD the kernel is compiled for (the register budget: 4 waves =
 // 128 VGPRs).  The one-level engine fits 128 with a 4-VGPR spill and runs 7%
 // faster at 4 resident waves than at 3 (150 VGPRs); the deeper hierarchies
@@ -627,6 +629,31 @@ __device__ __forceinline__ void ring_from_lds(int slot, RingView& v) {
     v = RingView{a.x, a.y, b.x, b.y};
 }
 
+// LDS-DMA of one 16-B (X4) or 4-B (X1) piece per active lane to lds + 16*lane
+// (X4) / 4*lane (X1).  lgkmcnt(0) first: earlier ds_reads of the target are done.
+template <bool X4>
+__device__ __forceinline__ void lds_dma(const AS1 char* src, uint32_t lds_base) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(lds_base);
+    unsigned keep;
+    if (X4)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(src), "s"(lo) : "memory");
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(src), "s"(lo) : "memory");
+}
+template <class T>
+__device__ __forceinline__ uint32_t lds_addr(T* p) {
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)p;
+}
+
+// The request's home directory set, staged before the request transmit (lane
+// w = way w: bytes 0-15 and the two dwords of the sharer word).  Up to 32 ways.
+static __shared__ v4u32 lds_dir_a[32];
+static __shared__ uint32_t lds_dir_w[2][32];
+
 // Network::transmit (network.cpp:97-160).  Inlined (a call would wait for every
 // outstanding store at entry and reload a spilled register at exit); every
 // argument is made wave-uniform so the hop loop runs on SGPRs and scalar
@@ -1153,13 +1180,30 @@ struct Engine {
     // end: nothing reached from here touches directory lines.  Every branch
     // that messages other caches does so first, at timer + access_time, so
     // the branch only chooses the probe; `probe` runs it.
-    __device__ int access_home(int cid, int home, const Req& r, int64_t timer, uint32_t* out_state) {
+    // Stage the home set of `addr` into LDS (lane w = way w) before the request
+    // transmit; 0 when the set is too wide to stage.  The caller tells
+    // access_home whether the transmit ran hops (2: it did not).
+    __device__ __forceinline__ int dir_stage(int home, uint64_t addr, bool no_hops) const {
+        const DirGeo& D = g->dir;
+        if (D.nways > 32) return 0;
+        const uint64_t set = set_index(addr, D.offbits, D.nsets);
+        const uint64_t line0 = ((uint64_t)home * D.csets + (set >> D.cset_shift)) * D.nways;
+        if ((uint64_t)ln < D.nways) {
+            const AS1 char* lp = (const AS1 char*)(const char*)(at<DirLine>(D.off_line) + line0 + (uint64_t)ln);
+            lds_dma<true>(lp, lds_addr(&lds_dir_a[0]));
+            lds_dma<false>(lp + 16, lds_addr(&lds_dir_w[0][0]));
+            lds_dma<false>(lp + 20, lds_addr(&lds_dir_w[1][0]));
+        }
+        return no_hops ? 2 : 1;
+    }
+    __device__ int access_home(int cid, int home, const Req& r, int64_t timer, uint32_t* out_state, int staged = 0) {
         PROF_T(p0);
-        int d = access_home_impl(cid, home, r, timer, out_state);
+        int d = access_home_impl(cid, home, r, timer, out_state, staged);
         PROF_ADD(PF_HOME, p0);
         return d;
     }
-    __device__ int access_home_impl(int cid, int home, const Req& r, int64_t timer, uint32_t* out_state) {
+    __device__ int access_home_impl(int cid, int home, const Req& r, int64_t timer, uint32_t* out_state,
+                                    int staged) {
         PROF_T(p_ld);
         const DirGeo& D = g->dir;
         const bool shared = g->shared_llc != 0;
@@ -1172,7 +1216,19 @@ struct Engine {
         const uint64_t line0 = ((uint64_t)home * D.csets + (set >> D.cset_shift)) * D.nways;   // reachable sets only
         const bool mine = (uint64_t)ln < D.nways;
         DirLine m;
-        if (mine) {
+        if (staged == 1) {
+            // staged before a transmit that ran hops: it issued at least 8 vector-
+            // memory operations since (4 header loads, 4 header stores)
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else if (staged == 2) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (mine && staged) {
+            const v4u32 a = lds_dir_a[ln];
+            m.tag = u64of(a.x, a.y);
+            m.ts = (int64_t)u64of(a.z, a.w);
+            m.w = u64of(lds_dir_w[0][ln], lds_dir_w[1][ln]);
+        } else if (mine) {
             m = lines[line0 + (uint64_t)ln];
         } else {
             m.tag = 0; m.ts = INT64_MAX; m.w = 0;
@@ -1419,11 +1475,15 @@ struct Engine {
                 const int home = wb ? wb_home : req_home;
                 const int src = leg == 2 ? home : cid, dst = leg == 2 ? cid : home;
                 const int len = wb ? (int)L.block : (leg == 1 ? 0 : req_reply);
+                // the request's home set is fetched while the request travels
+                // (nothing on the way writes directory lines; the write-back's
+                // home access, which may, is done)
+                const int staged = leg == 1 ? dir_stage(home, r.addr, src == dst) : 0;
                 const int d1 = (int)transmit(src, dst, len, (uint64_t)(timer + dly));
                 if (!wb) dly += d1;
                 if (leg == 2) break;
                 uint32_t hs;
-                const int d2 = access_home(cid, home, wb ? wb_req : r, timer + dly, &hs);
+                const int d2 = access_home(cid, home, wb ? wb_req : r, timer + dly, &hs, staged);
                 if (!wb) {
                     dly += d2;
                     if (is_miss) ret = hs;
@@ -1804,6 +1864,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PU_MIN_WAVES
         __builtin_amdgcn_wave_barrier();
         PROF_ADD(PF_LOOP, p_loop);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no staging DMA outlives the wave
     if (e.ln == 0) {
         if (pos) pos[blockIdx.x] = i;
         rs->batch_delay = lds_ctl.D;
