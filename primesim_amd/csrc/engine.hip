@@ -446,28 +446,55 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
     return d;
 }
 
+// Latency mode (LH): a launch with at most one replica per CU keeps every
+// queue header of its replica in the CU's LDS for the whole launch (copied in
+// at the start, back at the end), so the header round trip of each route
+// window becomes an LDS read.  136 KB: 2,176 queues (a 32x32 mesh has 1,984).
+#define PU_LDS_QHDR_BYTES (136 * 1024)
+#define AS3 __attribute__((address_space(3)))
+static __shared__ v4u32 lds_qhdr[PU_LDS_QHDR_BYTES / 16];
+template <bool LH>
+__device__ __forceinline__ uint32_t* hdr_ptr(const NetCtx& c, int q) {
+    if constexpr (LH) return reinterpret_cast<uint32_t*>(&lds_qhdr[(size_t)q * 4]);
+    else return (uint32_t*)(AS1 uint32_t*)q_hdr(c, q);
+}
+
 // Header write-back of queue q by the calling lane(s).
+template <bool LH>
 __device__ __forceinline__ void q_store_hdr(const NetCtx& c, int q, const QState& st) {
-    AS1 uint32_t* H = q_hdr(c, q);
     uint64_t sb = (uint64_t)__double_as_longlong(st.sum), qb = (uint64_t)__double_as_longlong(st.sum_sq);
-    *reinterpret_cast<AS1 v4u32*>(H) = v4u32{st.head, st.count, (uint32_t)st.n, (uint32_t)(st.n >> 32)};
-    *reinterpret_cast<AS1 v4u32*>(H + 4) = v4u32{(uint32_t)sb, (uint32_t)(sb >> 32), (uint32_t)qb, (uint32_t)(qb >> 32)};
-    *reinterpret_cast<AS1 v4u32*>(H + 8) = v4u32{(uint32_t)st.newest, (uint32_t)(st.newest >> 32), (uint32_t)st.f0,
-                                                 (uint32_t)(st.f0 >> 32)};
-    *reinterpret_cast<AS1 v2u32*>(H + 12) = v2u32{(uint32_t)st.f1, (uint32_t)(st.f1 >> 32)};
+    const v4u32 a = v4u32{st.head, st.count, (uint32_t)st.n, (uint32_t)(st.n >> 32)};
+    const v4u32 b = v4u32{(uint32_t)sb, (uint32_t)(sb >> 32), (uint32_t)qb, (uint32_t)(qb >> 32)};
+    const v4u32 cc = v4u32{(uint32_t)st.newest, (uint32_t)(st.newest >> 32), (uint32_t)st.f0, (uint32_t)(st.f0 >> 32)};
+    const v2u32 d = v2u32{(uint32_t)st.f1, (uint32_t)(st.f1 >> 32)};
+    if constexpr (LH) {
+        AS3 v4u32* H = (AS3 v4u32*)&lds_qhdr[(size_t)q * 4];
+        H[0] = a;
+        H[1] = b;
+        H[2] = cc;
+        *reinterpret_cast<AS3 v2u32*>(H + 3) = d;
+    } else {
+        AS1 uint32_t* H = q_hdr(c, q);
+        *reinterpret_cast<AS1 v4u32*>(H) = a;
+        *reinterpret_cast<AS1 v4u32*>(H + 4) = b;
+        *reinterpret_cast<AS1 v4u32*>(H + 8) = cc;
+        *reinterpret_cast<AS1 v2u32*>(H + 12) = d;
+    }
 }
 
 // M/G/1 update (queue_model_m_g_1.cpp:45-55) and header write-back (lane 0).
+template <bool LH>
 __device__ __forceinline__ void q_finish(const NetCtx& c, int q, QState& st, uint64_t t, uint64_t p, uint64_t d) {
     st.sum_sq = st.sum_sq + (double)p * (double)p;
     st.sum = st.sum + (double)p;
     st.n = st.n + 1;
     uint64_t fin = t + d + p;
     st.newest = fin > st.newest ? fin : st.newest;
-    if (lane_id() == 0) q_store_hdr(c, q, st);
+    if (lane_id() == 0) q_store_hdr<LH>(c, q, st);
 }
 
 // One computeQueueDelay on a uniform header (bus queues, unit tests).
+template <bool LH>
 __device__ __forceinline__ uint64_t q_step(const NetCtx& c, int q, QState& st, uint64_t t, uint64_t p, uint64_t minp,
                                            uint64_t& mg1, uint64_t& err) {
     if (st.count >= PU_QMAX) {      // prune the minimum (history_tree.cpp:49-55)
@@ -484,7 +511,7 @@ __device__ __forceinline__ uint64_t q_step(const NetCtx& c, int q, QState& st, u
         ring_load(c, q, st.head, st.count, v);
         d = tree_op(c, q, v, st.head, st.count, t, p, minp, err, st.f0, st.f1);
     }
-    q_finish(c, q, st, t, p, d);
+    q_finish<LH>(c, q, st, t, p, d);
     return d;
 }
 
@@ -502,21 +529,31 @@ __device__ __forceinline__ QState hdr_state(v4u32 a, v4u32 b, v4u32 c, v4u32 d) 
     return st;
 }
 __device__ __forceinline__ v4u32 uni4(v4u32 v) { return v4u32{uni32(v.x), uni32(v.y), uni32(v.z), uni32(v.w)}; }
+template <bool LH>
 __device__ __forceinline__ void hdr_load(const NetCtx& c, int q, v4u32& a, v4u32& b, v4u32& cc, v4u32& d) {
-    const AS1 v4u32* H = reinterpret_cast<const AS1 v4u32*>(q_hdr(c, q));
-    a = H[0];
-    b = H[1];
-    cc = H[2];
-    d = H[3];
+    if constexpr (LH) {
+        const AS3 v4u32* H = (const AS3 v4u32*)&lds_qhdr[(size_t)q * 4];
+        a = H[0];
+        b = H[1];
+        cc = H[2];
+        d = H[3];
+    } else {
+        const AS1 v4u32* H = reinterpret_cast<const AS1 v4u32*>(q_hdr(c, q));
+        a = H[0];
+        b = H[1];
+        cc = H[2];
+        d = H[3];
+    }
 }
 
 // A whole queue op loading its own state (bus queues, unit tests).
+template <bool LH>
 __device__ __forceinline__ uint64_t q_op(const NetCtx& c, int q, uint64_t t, uint64_t p, uint64_t minp, uint64_t& mg1,
                                          uint64_t& err) {
     v4u32 a, b, cc, d;
-    hdr_load(c, q, a, b, cc, d);
+    hdr_load<LH>(c, q, a, b, cc, d);
     QState st = hdr_state(uni4(a), uni4(b), uni4(cc), uni4(d));
-    return q_step(c, q, st, t, p, minp, mg1, err);
+    return q_step<LH>(c, q, st, t, p, minp, mg1, err);
 }
 
 // n / d for n < 2^16 as a multiply-high by m = ceil(2^32 / d) (exact there:
@@ -660,6 +697,7 @@ static __shared__ uint32_t lds_dir_w[2][32];
 // branches.  The protocol code reaches it from four sites only.
 // Lane h prefetches hop h's link header and the two interval starts at its
 // ring head; only hops taking the tree branch fetch their full ring.
+template <bool LH>
 __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char* base_in, int src, int dst, int len,
                                                  uint64_t timer) {
     NetCtx c;
@@ -706,7 +744,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         v4u32 ha = v4u32{0, 0, 0, 0}, hb = ha, hc = ha, hd = ha;
         if (h < hops) {
             rq = net_route_link(c, h, sx, sy, sz, rx, ry, rz, hx, hy);
-            hdr_load(c, rq, ha, hb, hc, hd);
+            hdr_load<LH>(c, rq, ha, hb, hc, hd);
         }
         // Everything about hop h that does not depend on its arrival time is
         // computed by lane h here, once per window: the prune (history_tree.cpp:
@@ -819,7 +857,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
             st.sum = st.sum + (double)plen;
             st.n = st.n + 1;
             st.newest = vfin > st.newest ? vfin : st.newest;
-            q_store_hdr(c, rq, st);
+            q_store_hdr<LH>(c, rq, st);
         }
         // No drain here: every staged ring was waited for when its hop consumed
         // it (predicted hops are a subset of the tree hops), and the header
@@ -847,7 +885,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
     return t - timer;
 }
 
-template <int NL>
+template <int NL, bool LH = false>
 struct Engine {
     const Geo* __restrict__ g;
     char* base;
@@ -884,7 +922,7 @@ struct Engine {
     }
     __device__ __forceinline__ uint64_t transmit(int src, int dst, int len, uint64_t timer) {
         PROF_T(p0);
-        uint64_t d = net_transmit(g, base, src, dst, len, timer);
+        uint64_t d = net_transmit<LH>(g, base, src, dst, len, timer);
         PROF_ADD(PF_NET, p0);
         return d;
     }
@@ -1389,7 +1427,7 @@ struct Engine {
         if (L.has_bus) {              // Bus::access (bus.cpp:55-61)
             stat_add(SN_BUSACC, 1);
             uint64_t bl = (uint64_t)g->bus_latency, mg1 = 0, err = 0;
-            int db = (int)q_op(net_ctx(), L.bus_q0 + cid, (uint64_t)(timer + dly), bl, bl, mg1, err);
+            int db = (int)q_op<LH>(net_ctx(), L.bus_q0 + cid, (uint64_t)(timer + dly), bl, bl, mg1, err);
             stat_add(SN_MG1, mg1);
             if (err) err_or(err);
             stat_add(SN_BUSCONT, (uint64_t)(int64_t)db);
@@ -1562,7 +1600,7 @@ struct Engine {
         if (L.has_bus) {              // Bus::access (bus.cpp:55-61)
             stat_add(SN_BUSACC, 1);
             uint64_t bl = (uint64_t)g->bus_latency, mg1 = 0, err = 0;
-            int db = (int)q_op(net_ctx(), L.bus_q0 + cid, (uint64_t)(timer + dly), bl, bl, mg1, err);
+            int db = (int)q_op<LH>(net_ctx(), L.bus_q0 + cid, (uint64_t)(timer + dly), bl, bl, mg1, err);
             stat_add(SN_MG1, mg1);
             if (err) err_or(err);
             stat_add(SN_BUSCONT, (uint64_t)(int64_t)db);
@@ -1766,8 +1804,8 @@ __device__ __forceinline__ void stats_init() {
 // replica of a fixed-size step.
 // SLICED is a separate instantiation so profiles list the time-sliced launches
 // (uncore_kernel<NL, true>) apart from fixed-range ones.
-template <int NL, bool SLICED>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PU_MIN_WAVES(NL)))) void uncore_kernel(const Geo* __restrict__ g, char* __restrict__ arena,
+template <int NL, bool SLICED, bool LH = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_MIN_WAVES(NL)))) void uncore_kernel(const Geo* __restrict__ g, char* __restrict__ arena,
                                                     int replica0, const pu_req* __restrict__ reqs,
                                                     const uint64_t* __restrict__ off,
                                                     int32_t* __restrict__ delays, uint64_t* __restrict__ pos,
@@ -1777,10 +1815,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PU_MIN_WAVES
         budget_ticks = 0;
     }
     const uint64_t wave_t0 = __builtin_amdgcn_s_memrealtime();
-    Engine<NL> e;
+    Engine<NL, LH> e;
     e.g = g;
     e.ln = lane_id();
     e.base = arena + (size_t)(replica0 + (int)blockIdx.x) * g->replica_bytes;
+    if constexpr (LH) {                                   // the replica's queue headers into LDS
+        const AS1 v4u32* gh = (const AS1 v4u32*)(AS1 char*)(e.base + g->off_qhdr);
+        const uint32_t nq4 = (uint32_t)g->nqueues * 4u;
+        for (uint32_t k = (uint32_t)e.ln; k < nq4; k += 64) lds_qhdr[k] = gh[k];
+    }
     stats_init();
     e.dly = 0;
     e.hit = false;
@@ -1865,6 +1908,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PU_MIN_WAVES
         PROF_ADD(PF_LOOP, p_loop);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no staging DMA outlives the wave
+    if constexpr (LH) {                                   // ... and back
+        __syncthreads();
+        AS1 v4u32* gh = (AS1 v4u32*)(AS1 char*)(e.base + g->off_qhdr);
+        const uint32_t nq4 = (uint32_t)g->nqueues * 4u;
+        for (uint32_t k = (uint32_t)e.ln; k < nq4; k += 64) gh[k] = lds_qhdr[k];
+    }
     if (e.ln == 0) {
         if (pos) pos[blockIdx.x] = i;
         rs->batch_delay = lds_ctl.D;
@@ -1929,7 +1978,7 @@ __global__ __launch_bounds__(64) void unit_queue_kernel(const Geo* __restrict__ 
     const NetCtx c = e.net_ctx();
     uint64_t calls = 0, err = 0;
     for (uint64_t i = 0; i < n; i++) {
-        uint64_t d = q_op(c, 0, t[i], p[i], minp, calls, err);
+        uint64_t d = q_op<false>(c, 0, t[i], p[i], minp, calls, err);
         if (e.ln == 0) out[i] = d;
     }
     if (e.ln == 0) *mg1 = calls;
@@ -2001,19 +2050,21 @@ extern "C" int pu_engine_unit_network(const Geo* d_geo, char* base, const int32_
 // ---------------------------------------------------------------- launchers
 extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,
                                 const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
-                                uint64_t budget_ticks, uint32_t flags, hipStream_t stream) {
+                                uint64_t budget_ticks, uint32_t flags, int lds_headers, hipStream_t stream) {
     dim3 grid((unsigned)nblocks), block(64);
+#define PU_LAUNCH3(L, S, H)                                                                                        \
+    hipLaunchKernelGGL((uncore_kernel<L, S, H>), grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays,   \
+                       pos, budget_ticks, flags)
 #define PU_LAUNCH(L)                                                                                              \
-    if (pos) hipLaunchKernelGGL((uncore_kernel<L, true>), grid, block, 0, stream, d_geo, arena, replica0, reqs, off, \
-                                delays, pos, budget_ticks, flags);                                               \
-    else hipLaunchKernelGGL((uncore_kernel<L, false>), grid, block, 0, stream, d_geo, arena, replica0, reqs, off,   \
-                            delays, pos, budget_ticks, flags);
+    if (pos) { if (lds_headers) PU_LAUNCH3(L, true, true); else PU_LAUNCH3(L, true, false); }                     \
+    else { if (lds_headers) PU_LAUNCH3(L, false, true); else PU_LAUNCH3(L, false, false); }
     switch (num_levels) {
         case 1: PU_LAUNCH(1); break;
         case 2: PU_LAUNCH(2); break;
         case 3: PU_LAUNCH(3); break;
         case 4: PU_LAUNCH(4); break;
 #undef PU_LAUNCH
+#undef PU_LAUNCH3
         default: return PU_EINVAL;
     }
     return hipGetLastError() == hipSuccess ? 0 : PU_EIO;
@@ -2035,6 +2086,9 @@ extern "C" int pu_engine_occupancy(int num_levels, int* blocks_per_cu) {
     *blocks_per_cu = n;
     return e == hipSuccess ? 0 : PU_EIO;
 }
+
+// Queue headers of one replica that fit the latency-mode LDS image.
+extern "C" int pu_engine_lds_header_queues(void) { return PU_LDS_QHDR_BYTES / (int)sizeof(QueueHdr); }
 
 extern "C" int pu_engine_init_queues(char* arena, uint64_t replica_bytes, uint64_t off_qhdr, uint64_t off_qring,
                                      int nqueues, int nreplicas, hipStream_t stream) {

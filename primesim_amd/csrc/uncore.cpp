@@ -32,7 +32,8 @@
 
 extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,
                                 const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
-                                uint64_t budget_ticks, uint32_t flags, hipStream_t stream);
+                                uint64_t budget_ticks, uint32_t flags, int lds_headers, hipStream_t stream);
+extern "C" int pu_engine_lds_header_queues(void);
 extern "C" int pu_engine_init_pool(char* arena, uint64_t replica_bytes, uint64_t off_pool_free, uint64_t off_run,
                                    int pool_entries, int nreplicas, hipStream_t stream);
 extern "C" int pu_engine_unit_queue(const Geo* d_geo, char* base, uint64_t minp, const uint64_t* t,
@@ -256,6 +257,8 @@ struct pu_handle {
     double last_ms = 0.0;
     struct timespec sim_start{}, sim_finish{};   // UncoreManager::sim_start_time / sim_finish_time
     uint32_t replay_flags = 0;   // PU_KF_CLOSED under PU_REPLAY_CLOSED
+    int cus = 0;                 // compute units of the device (latency-mode launches)
+    bool lds_headers_ok = false; // the replica's queue headers fit one CU's LDS
     // ThreadSched (thread_sched.cpp): the shared one, and per-replica copies
     // made on first use of a per-replica call (pu_*_core_replica: the server's
     // sessions); the shared calls update both
@@ -310,9 +313,12 @@ int ensure_stage(pu_handle* h, size_t n) {
 int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
            hipStream_t s, uint64_t* d_pos = nullptr, uint64_t budget_ticks = 0, uint32_t extra_flags = 0) {
     HIP_TRY(hipEventRecord(h->ev0, s), PU_EIO);
+    // latency mode: with at most one replica per CU each wave keeps its queue
+    // headers in the CU's LDS for the launch (engine.hip, LH)
+    const int lh = h->lds_headers_ok && nblocks <= h->cus ? 1 : 0;
     int rc = pu_engine_launch(h->d_geo, h->geo.num_levels, h->arena, replica0, nblocks, d_reqs, d_off, d_delay, d_pos,
                               budget_ticks, (extra_flags & PU_KF_NOHALT) ? extra_flags : (h->replay_flags | extra_flags),
-                              s);
+                              lh, s);
     if (rc) return pu::set_error(rc, "engine launch failed");
     HIP_TRY(hipEventRecord(h->ev1, s), PU_EIO);
     return 0;
@@ -442,6 +448,11 @@ pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device) {
         return nullptr;
     };
     if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice failed");
+    if (hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) h->cus = 0;
+    {
+        const char* e = std::getenv("PRIMEUNCORE_LDS_HEADERS");   // "0" turns latency mode off (A/B runs)
+        h->lds_headers_ok = geo.nqueues <= pu_engine_lds_header_queues() && !(e && e[0] == '0');
+    }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream create failed");
     if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) return fail("event create failed");
     if (hipMalloc(&h->d_geo, sizeof(Geo)) != hipSuccess) return fail("hipMalloc(geo) failed");

@@ -37,3 +37,13 @@ def test_engine_reproduces_reference(name):
         assert um.report() == c.report
     finally:
         um.close()
+
+
+@pytest.mark.parametrize("name", ["c1_hot", "c4_allcores", "three_level", "l2_shared_bus", "c5_prodcons_256",
+                                  "c4_closed"])
+def test_engine_global_header_mode(name, monkeypatch):
+    """The same goldens with the latency mode (queue headers in LDS, used by
+    launches of at most one replica per CU) turned off: the throughput kernel's
+    global-header path, which the bench runs, is pinned too."""
+    monkeypatch.setenv("PRIMEUNCORE_LDS_HEADERS", "0")
+    test_engine_reproduces_reference(name)
