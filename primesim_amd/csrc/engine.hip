@@ -167,20 +167,24 @@ __device__ unsigned long long g_blk_t0[PU_PROF_BLOCKS], g_blk_t1[PU_PROF_BLOCKS]
 #endif
 
 // Wave-uniform context of the queue/network code (all values in SGPRs).
+// Narrow on purpose: it stays live across the whole transmit, and SGPRs are the
+// engine's scarcest resource (each one spilled costs a v_writelane/v_readlane).
+// Delays are < 2^31 (checked at pu_create); the magics are < 2^32 for w >= 2
+// (a 1-node mesh never routes).
 struct NetCtx {
-    AS1 char* base;            // replica arena
-    uint64_t off_qhdr, off_qring;
-    uint64_t router, link_delay, inject;
+    AS1 char* qhdr;            // the replica's queue headers
+    AS1 char* qring;           // ... and rings
+    uint32_t router, link_delay, inject;
     int header_flits, data_width, w, net_type;
-    uint64_t w_magic, w2_magic;
+    uint32_t w_magic, w2_magic;
     int w2, blk_len, plen_blk;
 };
 
 __device__ __forceinline__ AS1 v2u64* q_ring(const NetCtx& c, int q) {
-    return reinterpret_cast<AS1 v2u64*>(c.base + c.off_qring) + (size_t)q * PU_QRING;
+    return reinterpret_cast<AS1 v2u64*>(c.qring) + (size_t)q * PU_QRING;
 }
 __device__ __forceinline__ AS1 uint32_t* q_hdr(const NetCtx& c, int q) {
-    return reinterpret_cast<AS1 uint32_t*>(c.base + c.off_qhdr + (uint64_t)q * sizeof(QueueHdr));
+    return reinterpret_cast<AS1 uint32_t*>(c.qhdr + (uint64_t)q * sizeof(QueueHdr));
 }
 
 // Load the `cnt` live slots of ring q starting at `head` (lane l holds slots l
@@ -558,7 +562,7 @@ __device__ __forceinline__ uint64_t q_op(const NetCtx& c, int q, uint64_t t, uin
 
 // n / d for n < 2^16 as a multiply-high by m = ceil(2^32 / d) (exact there:
 // n * (m*d - 2^32) < 2^32); uniform operands stay on the scalar unit.
-__device__ __forceinline__ uint32_t div_magic(uint32_t n, uint64_t m) { return (uint32_t)(((uint64_t)n * m) >> 32); }
+__device__ __forceinline__ uint32_t div_magic(uint32_t n, uint32_t m) { return (uint32_t)(((uint64_t)n * m) >> 32); }
 __device__ __forceinline__ void net_coords(const NetCtx& c, int id, int& x, int& y, int& z) {
     const uint32_t w = (uint32_t)c.w;
     if (c.net_type == 1) {
@@ -701,18 +705,18 @@ template <bool LH>
 __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char* base_in, int src, int dst, int len,
                                                  uint64_t timer) {
     NetCtx c;
-    c.base = (AS1 char*)(char*)uni64((uint64_t)base_in);
-    c.off_qhdr = g->off_qhdr;
-    c.off_qring = g->off_qring;
-    c.router = g->router_delay;
-    c.link_delay = g->link_delay;
-    c.inject = g->inject_delay;
+    AS1 char* base = (AS1 char*)(char*)uni64((uint64_t)base_in);
+    c.qhdr = base + g->off_qhdr;
+    c.qring = base + g->off_qring;
+    c.router = (uint32_t)g->router_delay;
+    c.link_delay = (uint32_t)g->link_delay;
+    c.inject = (uint32_t)g->inject_delay;
     c.header_flits = g->header_flits;
     c.data_width = g->data_width;
     c.w = g->net_width;
     c.net_type = g->net_type;
-    c.w_magic = g->w_magic;
-    c.w2_magic = g->w2_magic;
+    c.w_magic = (uint32_t)g->w_magic;
+    c.w2_magic = (uint32_t)g->w2_magic;
     c.w2 = g->w2;
     c.blk_len = g->blk_len;
     c.plen_blk = g->plen_blk;
@@ -908,12 +912,11 @@ struct Engine {
     // ------------------------------------------------------------ network
     __device__ __forceinline__ NetCtx net_ctx() const {
         NetCtx c;
-        c.base = (AS1 char*)base;
-        c.off_qhdr = g->off_qhdr;
-        c.off_qring = g->off_qring;
-        c.router = g->router_delay;
-        c.link_delay = g->link_delay;
-        c.inject = g->inject_delay;
+        c.qhdr = (AS1 char*)base + g->off_qhdr;
+        c.qring = (AS1 char*)base + g->off_qring;
+        c.router = (uint32_t)g->router_delay;
+        c.link_delay = (uint32_t)g->link_delay;
+        c.inject = (uint32_t)g->inject_delay;
         c.header_flits = g->header_flits;
         c.data_width = g->data_width;
         c.w = g->net_width;

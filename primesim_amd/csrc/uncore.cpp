@@ -139,6 +139,9 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
         return pu::set_error(PU_EINVAL, "limited-pointer broadcast needs one LLC per core (system.cpp:623)");
     if (!bus_sys && y.network.link_delay < 1) return pu::set_error(PU_EINVAL, "link_delay must be >= 1");
     if (y.network.data_width < 1) return pu::set_error(PU_EINVAL, "data_width must be >= 1");
+    if (y.network.router_delay >= (1ull << 31) || y.network.link_delay >= (1ull << 31) ||
+        y.network.inject_delay >= (1ull << 31))
+        return pu::set_error(PU_ENOTSUP, "router/link/inject delays must be < 2^31 cycles");
     g->home_offbits = ilog2(dc.block_size);
     g->home_mask_bits = (int)std::ceil(std::log2((double)N));
     {
