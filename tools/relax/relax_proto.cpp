@@ -20,7 +20,8 @@
 // Fixed point: every visit's L delay == the guess T used, and every stamp T
 // produced == the stamp F used.  Then the window equals the sequential run.
 //
-// usage: relax_proto PREFIX N_CORES WINDOW [max_sweeps]
+// usage: relax_proto PREFIX N_CORES WINDOW [max_sweeps] [guess mode 0|1] [bands]
+// (bands > 0: print the home-tile band statistics of the first sweep and exit)
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -388,6 +389,7 @@ int main(int argc, char** argv) {
     size_t W = (size_t)std::atol(argv[3]);
     int max_sweeps = argc > 4 ? std::atoi(argv[4]) : 10000;
     int mode = argc > 5 ? std::atoi(argv[5]) : 1;
+    const int bands = argc > 6 ? std::atoi(argv[6]) : 0;   // > 0: home-tile band statistics of sweep 1
     std::vector<Req> reqs;
     std::vector<int32_t> want;
     {
@@ -472,6 +474,32 @@ int main(int argc, char** argv) {
                 stampH[i] = sH;
                 dly[i] = d;
                 D += d - 1;
+            }
+            if (bands > 0 && sweep == 1) {
+                // SURVEY §8e's partition: the mesh's rows in `bands` bands (one per GPU);
+                // a link belongs to the band of its lower-row endpoint.  Every change of
+                // band along a request's visit sequence is a dependent hand-off between
+                // GPUs; so is the end of a request whose last visit is not in the band
+                // of the next request's first visit.
+                auto band_of = [&](int li) {
+                    // link index a*2w + b (network.cpp:213-307): X links have b = y,
+                    // Y links have a = the lower endpoint's y
+                    const int a = li / (2 * C.w), b = li % (2 * C.w);
+                    const int y = b < C.w ? b : a;
+                    return y * bands / C.w;
+                };
+                long cross = 0, single = 0, visits_all = 0;
+                for (size_t i2 = 0; i2 < wn; i2++) {
+                    const auto& vl = vlink[i2];
+                    visits_all += (long)vl.size();
+                    int changes = 0;
+                    for (size_t k = 1; k < vl.size(); k++) changes += band_of(vl[k]) != band_of(vl[k - 1]);
+                    cross += changes;
+                    single += changes == 0;
+                }
+                std::printf("bands %d: %.2f band changes per request (%.1f link visits), %.1f%% of requests in one band\n",
+                            bands, (double)cross / wn, (double)visits_all / wn, 100.0 * single / wn);
+                return 0;
             }
             // L
             lwork = lbase;
