@@ -95,7 +95,7 @@ struct QState {
     uint64_t n;
     double sum, sum_sq;
     uint64_t newest;
-    uint64_t f0, f1;
+    uint64_t f0;
 };
 
 #define AS1 __attribute__((address_space(1)))
@@ -459,7 +459,7 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
 static __shared__ v4u32 lds_qhdr[PU_LDS_QHDR_BYTES / 16];
 template <bool LH>
 __device__ __forceinline__ uint32_t* hdr_ptr(const NetCtx& c, int q) {
-    if constexpr (LH) return reinterpret_cast<uint32_t*>(&lds_qhdr[(size_t)q * 4]);
+    if constexpr (LH) return reinterpret_cast<uint32_t*>(&lds_qhdr[(size_t)q * 3]);
     else return (uint32_t*)(AS1 uint32_t*)q_hdr(c, q);
 }
 
@@ -470,19 +470,16 @@ __device__ __forceinline__ void q_store_hdr(const NetCtx& c, int q, const QState
     const v4u32 a = v4u32{st.head, st.count, (uint32_t)st.n, (uint32_t)(st.n >> 32)};
     const v4u32 b = v4u32{(uint32_t)sb, (uint32_t)(sb >> 32), (uint32_t)qb, (uint32_t)(qb >> 32)};
     const v4u32 cc = v4u32{(uint32_t)st.newest, (uint32_t)(st.newest >> 32), (uint32_t)st.f0, (uint32_t)(st.f0 >> 32)};
-    const v2u32 d = v2u32{(uint32_t)st.f1, (uint32_t)(st.f1 >> 32)};
     if constexpr (LH) {
-        AS3 v4u32* H = (AS3 v4u32*)&lds_qhdr[(size_t)q * 4];
+        AS3 v4u32* H = (AS3 v4u32*)&lds_qhdr[(size_t)q * 3];
         H[0] = a;
         H[1] = b;
         H[2] = cc;
-        *reinterpret_cast<AS3 v2u32*>(H + 3) = d;
     } else {
         AS1 uint32_t* H = q_hdr(c, q);
         *reinterpret_cast<AS1 v4u32*>(H) = a;
         *reinterpret_cast<AS1 v4u32*>(H + 4) = b;
         *reinterpret_cast<AS1 v4u32*>(H + 8) = cc;
-        *reinterpret_cast<AS1 v2u32*>(H + 12) = d;
     }
 }
 
@@ -501,11 +498,6 @@ __device__ __forceinline__ void q_finish(const NetCtx& c, int q, QState& st, uin
 template <bool LH>
 __device__ __forceinline__ uint64_t q_step(const NetCtx& c, int q, QState& st, uint64_t t, uint64_t p, uint64_t minp,
                                            uint64_t& mg1, uint64_t& err) {
-    if (st.count >= PU_QMAX) {      // prune the minimum (history_tree.cpp:49-55)
-        st.head = (st.head + 1) & (PU_QRING - 1);
-        st.count--;
-        st.f0 = st.f1;
-    }
     uint64_t d;
     if (st.f0 > t + p) {             // older than the tracked history: M/G/1 (history_tree.cpp:58-63)
         d = mg1_wait(st);
@@ -513,14 +505,20 @@ __device__ __forceinline__ uint64_t q_step(const NetCtx& c, int q, QState& st, u
     } else {
         RingView v;
         ring_load(c, q, st.head, st.count, v);
-        d = tree_op(c, q, v, st.head, st.count, t, p, minp, err, st.f0, st.f1);
+        uint64_t f1;
+        d = tree_op(c, q, v, st.head, st.count, t, p, minp, err, st.f0, f1);
+        if (st.count >= PU_QMAX) {   // the next call's prune (history_tree.cpp:49-55), done now
+            st.head = (st.head + 1) & (PU_QRING - 1);
+            st.count--;
+            st.f0 = f1;
+        }
     }
     q_finish<LH>(c, q, st, t, p, d);
     return d;
 }
 
 __device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
-__device__ __forceinline__ QState hdr_state(v4u32 a, v4u32 b, v4u32 c, v4u32 d) {
+__device__ __forceinline__ QState hdr_state(v4u32 a, v4u32 b, v4u32 c) {
     QState st;
     st.head = a.x;
     st.count = a.y;
@@ -529,24 +527,21 @@ __device__ __forceinline__ QState hdr_state(v4u32 a, v4u32 b, v4u32 c, v4u32 d) 
     st.sum_sq = __longlong_as_double((long long)u64of(b.z, b.w));
     st.newest = u64of(c.x, c.y);
     st.f0 = u64of(c.z, c.w);
-    st.f1 = u64of(d.x, d.y);
     return st;
 }
 __device__ __forceinline__ v4u32 uni4(v4u32 v) { return v4u32{uni32(v.x), uni32(v.y), uni32(v.z), uni32(v.w)}; }
 template <bool LH>
-__device__ __forceinline__ void hdr_load(const NetCtx& c, int q, v4u32& a, v4u32& b, v4u32& cc, v4u32& d) {
+__device__ __forceinline__ void hdr_load(const NetCtx& c, int q, v4u32& a, v4u32& b, v4u32& cc) {
     if constexpr (LH) {
-        const AS3 v4u32* H = (const AS3 v4u32*)&lds_qhdr[(size_t)q * 4];
+        const AS3 v4u32* H = (const AS3 v4u32*)&lds_qhdr[(size_t)q * 3];
         a = H[0];
         b = H[1];
         cc = H[2];
-        d = H[3];
     } else {
         const AS1 v4u32* H = reinterpret_cast<const AS1 v4u32*>(q_hdr(c, q));
         a = H[0];
         b = H[1];
         cc = H[2];
-        d = H[3];
     }
 }
 
@@ -554,9 +549,9 @@ __device__ __forceinline__ void hdr_load(const NetCtx& c, int q, v4u32& a, v4u32
 template <bool LH>
 __device__ __forceinline__ uint64_t q_op(const NetCtx& c, int q, uint64_t t, uint64_t p, uint64_t minp, uint64_t& mg1,
                                          uint64_t& err) {
-    v4u32 a, b, cc, d;
-    hdr_load<LH>(c, q, a, b, cc, d);
-    QState st = hdr_state(uni4(a), uni4(b), uni4(cc), uni4(d));
+    v4u32 a, b, cc;
+    hdr_load<LH>(c, q, a, b, cc);
+    QState st = hdr_state(uni4(a), uni4(b), uni4(cc));
     return q_step<LH>(c, q, st, t, p, minp, mg1, err);
 }
 
@@ -741,29 +736,25 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         PROF_T(p_setup);
         PROF_CNT(PF_WINDOWS, 1);
         // ---- prefetch the window: lane h = hop b0+h loads its link's header
-        // (one 64-B line: moments, ring cursor, first two interval starts)
+        // (48 B: moments, ring cursor, the first interval start)
         const int h = b0 + ln;
         const int nh = hops - b0 < 64 ? hops - b0 : 64;
         int rq = 0;
-        v4u32 ha = v4u32{0, 0, 0, 0}, hb = ha, hc = ha, hd = ha;
+        v4u32 ha = v4u32{0, 0, 0, 0}, hb = ha, hc = ha;
         if (h < hops) {
             rq = net_route_link(c, h, sx, sy, sz, rx, ry, rz, hx, hy);
-            hdr_load<LH>(c, rq, ha, hb, hc, hd);
+            hdr_load<LH>(c, rq, ha, hb, hc);
         }
         // Everything about hop h that does not depend on its arrival time is
-        // computed by lane h here, once per window: the prune (history_tree.cpp:
-        // 49-55), the front interval, the M/G/1 wait from the pre-update moments
-        // (queue_model_m_g_1.cpp:16-42) and the moment updates of q_finish.  The
-        // route's links are distinct, so no hop sees another hop's update.
-        const QState hs = hdr_state(ha, hb, hc, hd);
+        // computed by lane h here, once per window: the front interval (the
+        // prune of a full history was applied when it filled), the M/G/1 wait
+        // from the pre-update moments (queue_model_m_g_1.cpp:16-42) and the
+        // moment updates of q_finish.  The route's links are distinct, so no
+        // hop sees another hop's update.
+        const QState hs = hdr_state(ha, hb, hc);
         uint32_t vhead = hs.head, vcnt = hs.count;
-        uint64_t vf0 = hs.f0, vf1 = hs.f1;
-        if (vcnt >= PU_QMAX) {
-            vhead = (vhead + 1) & (PU_QRING - 1);
-            vcnt--;
-            vf0 = hs.f1;
-        }
-        const uint64_t vfront = vf0;    // post-prune minimum: the M/G/1 test
+        uint64_t vf0 = hs.f0;
+        const uint64_t vfront = vf0;    // the tree's minimum: the M/G/1 test
         uint64_t vd = ln < nh ? mg1_wait(hs) : 0;   // hop h's queue delay if it takes M/G/1
         uint64_t vfin = 0;              // t + d + p of hop h
         // Hop j arrives no earlier than LB_j = t + (j+1)*router + j*link_delay
@@ -830,6 +821,11 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                 ring_load(c, q, head, cnt, v);
             }
             d = tree_op(c, q, v, head, cnt, tj, (uint64_t)plen, c.link_delay, err, f0n, f1n);
+            if (cnt >= PU_QMAX) {               // the next call's prune (history_tree.cpp:49-55), done now
+                head = (head + 1) & (PU_QRING - 1);
+                cnt--;
+                f0n = f1n;
+            }
             if (staged && mi) {                 // keep PF rings in flight
                 PROF_T(p_r);
                 const int jj = (int)__builtin_ctzll(mi);
@@ -841,7 +837,6 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
             vhead = wl32(vhead, head, jt);
             vcnt = wl32(vcnt, cnt, jt);
             vf0 = wl64(vf0, f0n, jt);
-            vf1 = wl64(vf1, f1n, jt);
             vd = wl64(vd, d, jt);
             vfin = wl64(vfin, tj + d + (uint64_t)plen, jt);
             t = tj + d + c.link_delay;
@@ -856,7 +851,6 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
             st.head = vhead;
             st.count = vcnt;
             st.f0 = vf0;
-            st.f1 = vf1;
             st.sum_sq = st.sum_sq + (double)plen * (double)plen;
             st.sum = st.sum + (double)plen;
             st.n = st.n + 1;
@@ -1824,7 +1818,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
     e.base = arena + (size_t)(replica0 + (int)blockIdx.x) * g->replica_bytes;
     if constexpr (LH) {                                   // the replica's queue headers into LDS
         const AS1 v4u32* gh = (const AS1 v4u32*)(AS1 char*)(e.base + g->off_qhdr);
-        const uint32_t nq4 = (uint32_t)g->nqueues * 4u;
+        const uint32_t nq4 = (uint32_t)g->nqueues * (uint32_t)(sizeof(QueueHdr) / 16);
         for (uint32_t k = (uint32_t)e.ln; k < nq4; k += 64) lds_qhdr[k] = gh[k];
     }
     stats_init();
@@ -1914,7 +1908,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
     if constexpr (LH) {                                   // ... and back
         __syncthreads();
         AS1 v4u32* gh = (AS1 v4u32*)(AS1 char*)(e.base + g->off_qhdr);
-        const uint32_t nq4 = (uint32_t)g->nqueues * 4u;
+        const uint32_t nq4 = (uint32_t)g->nqueues * (uint32_t)(sizeof(QueueHdr) / 16);
         for (uint32_t k = (uint32_t)e.ln; k < nq4; k += 64) gh[k] = lds_qhdr[k];
     }
     if (e.ln == 0) {
@@ -1959,8 +1953,6 @@ __global__ void init_queues_kernel(char* arena, uint64_t replica_bytes, uint64_t
     h->sum_sq = 0.0;
     h->newest = 0;
     h->f0 = 0;
-    h->f1 = 0;
-    h->_pad = 0;
     QueueSlot* ring = reinterpret_cast<QueueSlot*>(base + off_qring) + q * PU_QRING;
     ring[0] = QueueSlot{0ull, UINT64_MAX};
 }

@@ -19,9 +19,9 @@
 //     pool     : pool_entries x nwords x u64 bitmaps + a free stack
 //     dalive, dcnt : per slice
 //   queues (Graphite history tree restated as a ring of sorted free intervals):
-//     qhdr : nqueues x QueueHdr (64 B, one line: M/G/1 moments, ring cursor and
-//            the first two interval starts, so the M/G/1-vs-tree decision of a
-//            hop needs this line only)  — links first, then per-cache buses
+//     qhdr : nqueues x QueueHdr (48 B: M/G/1 moments, ring cursor and the first
+//            interval start, so the M/G/1-vs-tree decision of a hop needs the
+//            header only)  — links first, then per-cache buses
 //     qring: nqueues x 128 x {first,second} (2 KB)
 //   stats (EngineStats), per-core completion cycles, run state.
 //
@@ -75,6 +75,11 @@ struct DirLine {
 #define PU_SH_POOL 0xFF
 #define PU_DIR_PROG_ESC 1023u
 
+// 48 B (three 16-B pieces): the prune of a full history (size >= 100 at the
+// start of computeQueueDelay, queue_model_history_tree.cpp:49-55) is applied
+// eagerly at the end of the tree op that fills it — nothing observes the tree
+// in between, and an M/G/1 visit never grows it — so the header needs the
+// tree's minimum (the M/G/1 test) but not the one after it.
 struct QueueHdr {
     uint32_t head;
     uint32_t count;
@@ -83,10 +88,6 @@ struct QueueHdr {
     double sum_sq;     // _sigma_service_time_square
     uint64_t newest;   // _newest_arrival_time
     uint64_t f0;       // ring[head].first: the tree's minimum key (the M/G/1 test)
-    uint64_t f1;       // ring[head+1].first: the minimum after a prune; valid
-                       // whenever count >= PU_QMAX (only a tree op raises count,
-                       // and it refreshes f0/f1 from the ring it holds)
-    uint64_t _pad;
 };
 
 struct QueueSlot {
@@ -182,3 +183,4 @@ struct RunState {
     int64_t msg_shift;     // PU_KF_CLOSED: the open message's core shift at its first request
     uint64_t dead_tags;    // PU_KF_MSGHALT: receive threads (pu_req.tag < 64) that have exited
 };
+static_assert(sizeof(QueueHdr) == 48, "QueueHdr is three 16-B pieces");
