@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <ctime>
 #include <cstddef>
@@ -262,16 +263,22 @@ struct pu_handle {
     uint32_t replay_flags = 0;   // PU_KF_CLOSED under PU_REPLAY_CLOSED
     int cus = 0;                 // compute units of the device (latency-mode launches)
     bool lds_headers_ok = false; // the replica's queue headers fit one CU's LDS
+    bool lds_headers_short = false;   // latency mode for short host batches too
     // ThreadSched (thread_sched.cpp): the shared one, and per-replica copies
     // made on first use of a per-replica call (pu_*_core_replica: the server's
     // sessions); the shared calls update both
     pu::Sched sched;
     std::vector<std::unique_ptr<pu::Sched>> rsched;
     pu::Sched& sched_of(int r) { return rsched[(size_t)r] ? *rsched[(size_t)r] : sched; }
-    // staging for host-buffer batches
+    // staging for host-buffer batches: one device block [offsets | requests]
+    // filled by one copy from a pinned host twin, and pinned landing slots for
+    // the delays and the replica's error flags
     pu_req* d_reqs = nullptr;
     int32_t* d_delays = nullptr;
     uint64_t* d_off = nullptr;
+    uint8_t* h_in = nullptr;     // pinned: [offsets (64 B) | reqs[cap]]
+    int32_t* h_delays = nullptr; // pinned: delays[cap]
+    uint64_t* h_tail = nullptr;  // pinned: error flags, RunState
     size_t stage_cap = 0;
     std::mutex mu;
 };
@@ -299,26 +306,68 @@ int reset_state(pu_handle* h) {
     return 0;
 }
 
-int ensure_stage(pu_handle* h, size_t n) {
-    if (n <= h->stage_cap && h->d_reqs) return 0;
-    size_t cap = n < 4096 ? 4096 : n;
-    if (h->d_reqs) (void)hipFree(h->d_reqs);
+constexpr size_t kOffBytes = 64;   // offsets, padded so the requests start on a cache line
+constexpr size_t kTailBytes = 8 + sizeof(RunState);
+constexpr size_t kShortBatch = 16384;   // host batches below this skip the LDS header image
+
+void free_stage(pu_handle* h) {
+    if (h->d_off) (void)hipFree(h->d_off);   // d_reqs lives in the same block
     if (h->d_delays) (void)hipFree(h->d_delays);
+    if (h->h_in) (void)hipHostFree(h->h_in);
+    if (h->h_delays) (void)hipHostFree(h->h_delays);
+    if (h->h_tail) (void)hipHostFree(h->h_tail);
+    h->d_off = nullptr;
     h->d_reqs = nullptr;
     h->d_delays = nullptr;
-    HIP_TRY(hipMalloc(&h->d_reqs, cap * sizeof(pu_req)), PU_ENOMEM);
+    h->h_in = nullptr;
+    h->h_delays = nullptr;
+    h->h_tail = nullptr;
+    h->stage_cap = 0;
+}
+
+int ensure_stage(pu_handle* h, size_t n) {
+    if (n <= h->stage_cap && h->d_off) return 0;
+    size_t cap = n < 4096 ? 4096 : n;
+    free_stage(h);
+    const size_t in_bytes = kOffBytes + cap * sizeof(pu_req);
+    void* p = nullptr;
+    HIP_TRY(hipMalloc(&p, in_bytes), PU_ENOMEM);
+    h->d_off = (uint64_t*)p;
+    h->d_reqs = (pu_req*)((uint8_t*)p + kOffBytes);
     HIP_TRY(hipMalloc(&h->d_delays, cap * sizeof(int32_t)), PU_ENOMEM);
-    if (!h->d_off) HIP_TRY(hipMalloc(&h->d_off, 2 * sizeof(uint64_t)), PU_ENOMEM);
+    HIP_TRY(hipHostMalloc((void**)&h->h_in, in_bytes, hipHostMallocDefault), PU_ENOMEM);
+    HIP_TRY(hipHostMalloc((void**)&h->h_delays, cap * sizeof(int32_t), hipHostMallocDefault), PU_ENOMEM);
+    HIP_TRY(hipHostMalloc((void**)&h->h_tail, kTailBytes, hipHostMallocDefault), PU_ENOMEM);
     h->stage_cap = cap;
     return 0;
 }
 
+// Wait for a short synchronous launch by polling: a blocking wait lets the
+// host thread sleep and it wakes well after the kernel ends (the
+// per-request API pays that on every call). Long launches fall back to the
+// blocking wait after a few milliseconds of polling.
+int wait_stream(hipStream_t s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) return 0;
+        if (e != hipErrorNotReady) return pu::set_error(PU_EIO, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+    }
+    HIP_TRY(hipStreamSynchronize(s), PU_EIO);
+    return 0;
+}
+
 int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
-           hipStream_t s, uint64_t* d_pos = nullptr, uint64_t budget_ticks = 0, uint32_t extra_flags = 0) {
+           hipStream_t s, uint64_t* d_pos = nullptr, uint64_t budget_ticks = 0, uint32_t extra_flags = 0,
+           bool short_launch = false) {
     HIP_TRY(hipEventRecord(h->ev0, s), PU_EIO);
     // latency mode: with at most one replica per CU each wave keeps its queue
-    // headers in the CU's LDS for the launch (engine.hip, LH)
-    const int lh = h->lds_headers_ok && nblocks <= h->cus ? 1 : 0;
+    // headers in the CU's LDS for the launch (engine.hip, LH). Copying the
+    // image in and out costs ~17 us a launch, more than a short host batch
+    // (a lone uncore_access, one MEM_REQUESTS message) wins back, so those
+    // run with the headers in HBM (tools/latency_bench.py)
+    const int lh = h->lds_headers_ok && nblocks <= h->cus && !short_launch ? 1 : 0;
     int rc = pu_engine_launch(h->d_geo, h->geo.num_levels, h->arena, replica0, nblocks, d_reqs, d_off, d_delay, d_pos,
                               budget_ticks, (extra_flags & PU_KF_NOHALT) ? extra_flags : (h->replay_flags | extra_flags),
                               lh, s);
@@ -453,8 +502,10 @@ pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device) {
     if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice failed");
     if (hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) h->cus = 0;
     {
-        const char* e = std::getenv("PRIMEUNCORE_LDS_HEADERS");   // "0" turns latency mode off (A/B runs)
+        // "0" turns latency mode off, "2" uses it for short host batches too (A/B runs, tests)
+        const char* e = std::getenv("PRIMEUNCORE_LDS_HEADERS");
         h->lds_headers_ok = geo.nqueues <= pu_engine_lds_header_queues() && !(e && e[0] == '0');
+        h->lds_headers_short = e && e[0] == '2';
     }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream create failed");
     if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) return fail("event create failed");
@@ -481,9 +532,7 @@ void pu_destroy(pu_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->arena) (void)hipFree(h->arena);
     if (h->d_geo) (void)hipFree(h->d_geo);
-    if (h->d_reqs) (void)hipFree(h->d_reqs);
-    if (h->d_delays) (void)hipFree(h->d_delays);
-    if (h->d_off) (void)hipFree(h->d_off);
+    free_stage(h);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -567,30 +616,45 @@ int pu_get_core_id_replica(pu_handle* h, int replica, int prog_id, int thread_id
 }
 
 namespace {
-int access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n, int32_t* delay_out, uint32_t extra) {
+int access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n, int32_t* delay_out, uint32_t extra,
+                 uint64_t* last_addr = nullptr) {
     if (!h || (!reqs && n)) return pu::set_error(PU_EINVAL, "bad arguments");
     if (replica < 0 || replica >= h->R) return pu::set_error(PU_ERANGE, "replica out of range");
     if (n == 0) return 0;
     std::lock_guard<std::mutex> lk(h->mu);
     int rc = ensure_stage(h, n);
     if (rc) return rc;
-    uint64_t off[2] = {0, (uint64_t)n};
-    HIP_TRY(hipMemcpyAsync(h->d_reqs, reqs, n * sizeof(pu_req), hipMemcpyHostToDevice, h->stream), PU_EIO);
-    HIP_TRY(hipMemcpyAsync(h->d_off, off, sizeof(off), hipMemcpyHostToDevice, h->stream), PU_EIO);
-    rc = launch(h, replica, 1, h->d_reqs, h->d_off, h->d_delays, h->stream, nullptr, 0, extra);
+    // one host-to-device copy of [offsets | requests] from pinned memory
+    const uint64_t off[2] = {0, (uint64_t)n};
+    std::memcpy(h->h_in, off, kOffBytes);
+    std::memcpy(h->h_in + kOffBytes, reqs, n * sizeof(pu_req));
+    HIP_TRY(hipMemcpyAsync(h->d_off, h->h_in, kOffBytes + n * sizeof(pu_req), hipMemcpyHostToDevice, h->stream),
+            PU_EIO);
+    rc = launch(h, replica, 1, h->d_reqs, h->d_off, h->d_delays, h->stream, nullptr, 0, extra,
+                n < kShortBatch && !h->lds_headers_short);
     if (rc) return rc;
     if (delay_out)
-        HIP_TRY(hipMemcpyAsync(delay_out, h->d_delays, n * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream), PU_EIO);
-    uint64_t ef = 0;
-    HIP_TRY(hipMemcpyAsync(&ef, h->arena + (size_t)replica * h->geo.replica_bytes + h->geo.off_stats +
-                                    offsetof(EngineStats, error_flags),
-                           sizeof(ef), hipMemcpyDeviceToHost, h->stream), PU_EIO);
-    HIP_TRY(hipStreamSynchronize(h->stream), PU_EIO);
+        HIP_TRY(hipMemcpyAsync(h->h_delays, h->d_delays, n * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream),
+                PU_EIO);
+    char* rbase = h->arena + (size_t)replica * h->geo.replica_bytes;
+    HIP_TRY(hipMemcpyAsync(h->h_tail, rbase + h->geo.off_stats + offsetof(EngineStats, error_flags), 8,
+                           hipMemcpyDeviceToHost, h->stream), PU_EIO);
+    if (last_addr)
+        HIP_TRY(hipMemcpyAsync(h->h_tail + 1, rbase + h->geo.off_run, sizeof(RunState), hipMemcpyDeviceToHost,
+                               h->stream), PU_EIO);
+    rc = wait_stream(h->stream);
+    if (rc) return rc;
+    if (delay_out) std::memcpy(delay_out, h->h_delays, n * sizeof(int32_t));
+    if (last_addr) {
+        RunState rs;
+        std::memcpy(&rs, h->h_tail + 1, sizeof(rs));
+        *last_addr = rs.last_addr;
+    }
     float ms = 0;
     if (hipEventElapsedTime(&ms, h->ev0, h->ev1) == hipSuccess) h->last_ms = ms;
     // an engine limit stopped the replica where the reference would continue:
     // the delays after that request are not the reference's, say so
-    return limit_error(ef, replica);
+    return limit_error(h->h_tail[0], replica);
 }
 }  // namespace
 
@@ -612,13 +676,9 @@ int pu_access(pu_handle* h, int core_id, int prog_id, int mem_type, uint64_t* ad
     int32_t d = 0;
     // UncoreManager::uncore_access has no prime.cpp halt rule (PU_KF_NOHALT); a
     // closed-loop shift would move the caller's timer, so it is never applied here
-    int rc = access_batch(h, 0, &r, 1, &d, PU_KF_NOHALT);
+    // with the TLB on, InsMem::addr_dmem comes back as the physical address (system.cpp:916)
+    int rc = access_batch(h, 0, &r, 1, &d, PU_KF_NOHALT, h->geo.tlb_enable ? addr : nullptr);
     if (rc) return rc;
-    if (h->geo.tlb_enable) {    // InsMem::addr_dmem now holds the physical address (system.cpp:916)
-        RunState rs;
-        HIP_TRY(hipMemcpy(&rs, h->arena + h->geo.off_run, sizeof(rs), hipMemcpyDeviceToHost), PU_EIO);
-        *addr = rs.last_addr;
-    }
     return d;
 }
 

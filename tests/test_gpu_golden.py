@@ -41,9 +41,12 @@ def test_engine_reproduces_reference(name):
 
 @pytest.mark.parametrize("name", ["c1_hot", "c4_allcores", "three_level", "l2_shared_bus", "c5_prodcons_256",
                                   "c4_closed"])
-def test_engine_global_header_mode(name, monkeypatch):
-    """The same goldens with the latency mode (queue headers in LDS, used by
-    launches of at most one replica per CU) turned off: the throughput kernel's
-    global-header path, which the bench runs, is pinned too."""
-    monkeypatch.setenv("PRIMEUNCORE_LDS_HEADERS", "0")
+@pytest.mark.parametrize("mode", ["0", "2"])
+def test_engine_header_modes(name, mode, monkeypatch):
+    """The same goldens with each queue-header placement forced: "0" keeps the
+    headers in HBM for every launch (the throughput kernel's path, which the
+    bench runs); "2" uses the latency mode (headers in LDS, launches of at most
+    one replica per CU) for short host batches too, which otherwise run with
+    the headers in HBM."""
+    monkeypatch.setenv("PRIMEUNCORE_LDS_HEADERS", mode)
     test_engine_reproduces_reference(name)

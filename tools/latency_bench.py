@@ -1,0 +1,80 @@
+"""Latency of the single-request and per-message paths (run on the GPU box).
+
+uncore_access (pu_access: one launch per request) and access_batch of one
+100-request message (pu_access_batch: one launch per message, prime.cpp's
+MEM_REQUESTS), on replica 0 of a C4 engine after a warm-up, wall-clock per call.
+
+    python tools/latency_bench.py [--calls 2000] [--out gpurun_out/latency.json]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--calls", type=int, default=2000)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    import primesim_amd as P
+    from primesim_amd import _abi as A
+    from primesim_amd import config as CF
+    cfg = P.config_from_dict(CF.preset("C4"))
+    spec = P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=4, num_quanta=2, max_requests=200_000 + 200 * a.calls)
+    reqs = P.generate_stream(spec)
+    um = P.UncoreManager()
+    um.init(cfg, replicas=1)
+    for prog, th in P.stream_threads(spec):
+        um.allocCore(prog, th)
+    um.access_batch(reqs[:100_000])                    # warm caches and link histories
+    i0 = 100_000
+    t0 = time.perf_counter()
+    for q in reqs[i0:i0 + a.calls]:
+        ins = P.InsMem(mem_type=int(q["mem_type"]), prog_id=int(q["prog_id"]), addr_dmem=int(q["addr"]))
+        um.uncore_access(int(q["core"]), ins, int(q["timer"]))
+    single = (time.perf_counter() - t0) / a.calls
+    i1 = i0 + a.calls
+    bs = np.flatnonzero(reqs["batch_start"][i1:]) + i1
+    nmsg = min(max(1, a.calls // 10), len(bs) - 1)
+    bounds = [(int(bs[k]), int(bs[k + 1])) for k in range(nmsg)]
+    kms = 0.0
+    t0 = time.perf_counter()
+    for s, e in bounds:
+        um.access_batch(reqs[s:e])
+        kms += um.last_kernel_ms()
+    per_msg = (time.perf_counter() - t0) / nmsg
+    n = sum(e - s for s, e in bounds)
+    res = {"uncore_access_us": single * 1e6, "message_us": per_msg * 1e6, "requests_per_message": n / nmsg,
+           "message_us_per_request": per_msg * 1e6 / (n / nmsg), "calls": a.calls,
+           "kernel_us_per_message": kms * 1e3 / nmsg,
+           "lds_headers_env": os.environ.get("PRIMEUNCORE_LDS_HEADERS", ""),
+           "library_source_hash": P.uncore.library_source_hash()}
+    # kernel time per request against the launch size (contiguous slices of the
+    # same stream): separates per-launch costs from the per-request chain
+    pos = bounds[-1][1]
+    sweep = {}
+    for size in (100, 1000, 10_000, 40_000):
+        e = int(bs[np.searchsorted(bs, pos + size)])
+        t0 = time.perf_counter()
+        um.access_batch(reqs[pos:e])
+        wall = time.perf_counter() - t0
+        sweep[str(size)] = {"requests": e - pos, "kernel_us_per_request": um.last_kernel_ms() * 1e3 / (e - pos),
+                            "wall_us_per_request": wall * 1e6 / (e - pos)}
+        pos = e
+    res["size_sweep"] = sweep
+    print(json.dumps(res))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+    um.close()
+
+
+if __name__ == "__main__":
+    main()
