@@ -6,7 +6,8 @@
  *     -> System::access           (reference src/system.cpp:144-168)
  * i.e. set-associative tag/LRU lookups (Cache), directory / shared-LLC MESI
  * transitions, XY mesh Network/Link timing with the Graphite history-tree +
- * M/G/1 queue model, and fixed-latency Dram.
+ * M/G/1 queue model, and fixed-latency Dram (or, opt-in, a DRAM bank model
+ * with no reference counterpart: pu_dram_cfg).
  *
  * Plain C: pointers, sizes and PODs only; no exceptions cross this boundary.
  * Every entry point returns 0 (or a non-negative value) on success and a
@@ -70,6 +71,26 @@ typedef struct pu_net_cfg {            /* XmlNetwork, xml_parser.h:57-65 */
     uint64_t inject_delay;
 } pu_net_cfg;
 
+/* DRAM bank timing (north_star stage 4).  Opt-in, no reference counterpart:
+ * the reference's Dram is a fixed latency plus a counter (dram.cpp:43-47), and
+ * banks = 0 (the default; a config without a <dram> element) is exactly that.
+ * With banks > 0 every Dram::access call site of System (system.cpp) becomes
+ * an access to one bank of an open-page DRAM at that call's cycle t:
+ *   row r = addr >> log2(row_bytes);  bank = r & (banks-1);  page = r >> log2(banks)
+ *   start = max(t, bank.ready)
+ *   act   = 0 (page open: row hit) | t_rcd (bank closed) | t_rp + t_rcd (other page open)
+ *   delay = (start - t) + act + dram_access_time
+ *   bank.ready = start + act + t_burst;  bank.open = page
+ * Call sites whose Dram::access delay the reference discards (write-backs)
+ * still occupy the bank.  banks and row_bytes are powers of two. */
+typedef struct pu_dram_cfg {
+    int32_t  banks;          /* 0 = fixed latency (the reference) */
+    int32_t  t_rcd;          /* activate to column command, cycles */
+    int32_t  t_rp;           /* precharge, cycles */
+    int32_t  t_burst;        /* cycles a bank stays busy after the column command */
+    uint64_t row_bytes;      /* bytes of one row (page) of one bank, >= 64 */
+} pu_dram_cfg;
+
 typedef struct pu_sys_cfg {            /* XmlSys, xml_parser.h:69-89 */
     int32_t  sys_type;                 /* 0 directory, 1 bus */
     int32_t  protocol_type;            /* 0 full map, 1 limited pointer */
@@ -89,6 +110,7 @@ typedef struct pu_sys_cfg {            /* XmlSys, xml_parser.h:69-89 */
     pu_cache_cfg directory_cache;
     pu_cache_cfg tlb_cache;
     pu_cache_cfg cache[PU_MAX_LEVELS];
+    pu_dram_cfg  dram;                 /* optional <dram> element; no XmlSys counterpart */
 } pu_sys_cfg;
 
 typedef struct pu_sim_cfg {            /* XmlSim, xml_parser.h:92-100 */
@@ -104,7 +126,9 @@ typedef struct pu_sim_cfg {            /* XmlSim, xml_parser.h:92-100 */
 /* Parse a config_prime XML file (schema of reference tools/config_prime:62-198;
  * replaces XmlParser::parse, reference src/xml_parser.cpp:684-718, including its
  * required-field counts 5/13/4/6/6/6*L and the optional max_num_sharers,
- * net_type and inject_delay).  Returns 0 or PU_EINVAL. */
+ * net_type and inject_delay).  An optional <dram> element inside <system>
+ * (banks, row_bytes, t_rcd, t_rp, t_burst) fills pu_sys_cfg.dram; the
+ * reference's parser ignores it.  Returns 0 or PU_EINVAL. */
 int pu_config_load_xml(const char* path, pu_sim_cfg* out);
 int pu_config_parse_xml(const char* text, size_t len, pu_sim_cfg* out);
 /* Write the config back out in config_prime's XML layout. */
@@ -165,6 +189,11 @@ typedef struct pu_stats {
     uint64_t bus_accesses;          /* Bus::access calls */
     uint64_t requests;              /* uncore_access calls */
     uint64_t error_flags;           /* PU_ERRF_* bits; 0 for a valid run */
+    /* DRAM bank model (pu_dram_cfg.banks > 0; all 0 otherwise) */
+    uint64_t dram_row_hits;         /* accesses to the open page of their bank */
+    uint64_t dram_row_empty;        /* accesses to a closed bank */
+    uint64_t dram_row_conflicts;    /* accesses that closed another page */
+    uint64_t dram_bank_wait;        /* cycles spent waiting for a busy bank */
 } pu_stats;
 
 #define PU_ERRF_CORE_RANGE   (1ull << 0)  /* core_id >= num_cores (system.cpp:147) */

@@ -14,6 +14,8 @@
 //                                    reference src/Graphite/queue_model_history_tree.cpp:42-125,
 //                                    queue_model_m_g_1.cpp:16-55
 //   Dram::access, PageTable::translate reference src/dram.cpp:43-47, page_table.cpp:56-72
+//     (+ the opt-in DRAM bank model of include/primeuncore.h pu_dram_cfg, which
+//     has no reference counterpart: its parity is engine vs this restatement)
 //   ThreadSched::allocCore            reference src/thread_sched.cpp:55-67
 // and the request loop of reference src/prime.cpp:120-137.
 //
@@ -220,6 +222,10 @@ struct Sys {
     std::vector<int64_t> core_shift;   // closed loop: the core's summed batch delays
     int64_t msg_shift = 0;             // closed loop: the open message's shift
     bool skip_msg = false;             // CPUREF_MSGHALT: the open message went negative
+    // opt-in DRAM bank model (pu_dram_cfg): per bank the cycle it is free and
+    // its open page + 1 (0 = closed)
+    std::vector<int64_t> bank_ready;
+    std::vector<uint64_t> bank_open;
 
     // -------------------------------------------------- geometry
     std::string init(const pu_sim_cfg* c) {
@@ -297,6 +303,12 @@ struct Sys {
         core_stat.assign((size_t)cores, 0);
         completion.assign((size_t)cores, -1);
         core_shift.assign((size_t)cores, 0);
+        const pu_dram_cfg& dm = y.dram;
+        if (dm.banks < 0 || (dm.banks & (dm.banks - 1)) != 0) return "dram banks must be 0 or a power of two";
+        if (dm.banks > 0 && (dm.row_bytes < 64 || (dm.row_bytes & (dm.row_bytes - 1)) != 0))
+            return "dram row_bytes must be a power of two >= 64";
+        bank_ready.assign((size_t)dm.banks, 0);
+        bank_open.assign((size_t)dm.banks, 0);
         return "";
     }
 
@@ -401,9 +413,33 @@ struct Sys {
         return hb % (1 << (hm - 1));
     }
 
-    int dram() {
+    // Dram::access at cycle t for address addr: fixed latency, or one
+    // open-page bank access under pu_dram_cfg (banks > 0; formula in
+    // include/primeuncore.h).  Sites whose delay System discards still occupy
+    // the bank.
+    int dram(uint64_t addr, int64_t t) {
         st.dram_accesses++;
-        return cfg.sys.dram_access_time;
+        const pu_dram_cfg& dm = cfg.sys.dram;
+        if (dm.banks == 0) return cfg.sys.dram_access_time;
+        const uint64_t row = addr / dm.row_bytes;
+        const size_t bank = (size_t)(row % (uint64_t)dm.banks);
+        const uint64_t page = row / (uint64_t)dm.banks + 1;
+        const int64_t start = std::max(t, bank_ready[bank]);
+        int64_t act;
+        if (bank_open[bank] == page) {
+            act = 0;
+            st.dram_row_hits++;
+        } else if (bank_open[bank] == 0) {
+            act = dm.t_rcd;
+            st.dram_row_empty++;
+        } else {
+            act = (int64_t)dm.t_rp + dm.t_rcd;
+            st.dram_row_conflicts++;
+        }
+        bank_ready[bank] = start + act + dm.t_burst;
+        bank_open[bank] = page;
+        st.dram_bank_wait += (uint64_t)(start - t);
+        return (int)(start - t + act) + cfg.sys.dram_access_time;
     }
 
     // -------------------------------------------------- downward propagation (system.cpp:488-572)
@@ -519,7 +555,7 @@ struct Sys {
                     delay += inval_down(last, own, o);
                     int reply = (!shared || s == M) ? blk : 0;
                     delay += (int)transmit(own, home, reply, (uint64_t)(timer + delay));
-                    dram();
+                    dram(old.addr, timer + delay);
                 } else if (s == S) {
                     delay += inval_sharers(d, li, home, o, timer + delay);
                 } else if (s == B) {
@@ -530,7 +566,7 @@ struct Sys {
             d.miss++;
             clear_sharers(d, li);
             add_sharer(d, li, cid);
-            delay += dram();
+            delay += dram(r.addr, timer + delay);
         } else if (li < 0) {
             // WB that misses at home: the reference dereferences NULL
             st.error_flags |= PU_ERRF_WB_MISS;
@@ -546,10 +582,10 @@ struct Sys {
                     delay += (int)transmit(own, home, blk, (uint64_t)(timer + delay));
                 } else if (s == S) {
                     delay += inval_sharers(d, li, home, r, timer + delay);
-                    if (!shared) delay += dram();
+                    if (!shared) delay += dram(r.addr, timer + delay);
                 } else if (s == B) {
                     delay += broadcast(home, r, timer + delay);
-                    if (!shared) delay += dram();
+                    if (!shared) delay += dram(r.addr, timer + delay);
                 }
                 d.st[(size_t)li] = M;
                 clear_sharers(d, li);
@@ -562,11 +598,11 @@ struct Sys {
                     delay += (int)transmit(own, home, blk, (uint64_t)(timer + delay));
                     d.st[(size_t)li] = S;
                 } else if (s == S) {
-                    if (!shared) delay += dram();
+                    if (!shared) delay += dram(r.addr, timer + delay);
                     bool lim = cfg.sys.protocol_type == 1 && count_sharers(d, li) >= cfg.sys.max_num_sharers;
                     d.st[(size_t)li] = lim ? B : S;
                 } else if (s == B) {
-                    if (!shared) delay += dram();
+                    if (!shared) delay += dram(r.addr, timer + delay);
                 } else if (s == V) {
                     d.st[(size_t)li] = E;
                 }
@@ -574,7 +610,7 @@ struct Sys {
             } else {
                 d.st[(size_t)li] = shared ? V : I;
                 clear_sharers(d, li);
-                dram();
+                dram(r.addr, timer + delay);
             }
         }
         uint8_t fs = d.st[(size_t)li];
@@ -745,7 +781,7 @@ struct Sys {
                 }
                 c.st[(size_t)li] = shared_line ? S : E;
             }
-            dly += dram();
+            dly += dram(r.addr, timer + dly);
         }
         c.miss++;
         return c.st[(size_t)li];

@@ -44,6 +44,13 @@ class NetCfg(C.Structure):
     ]
 
 
+class DramCfg(C.Structure):              # pu_dram_cfg (opt-in bank model)
+    _fields_ = [
+        ("banks", C.c_int32), ("t_rcd", C.c_int32), ("t_rp", C.c_int32), ("t_burst", C.c_int32),
+        ("row_bytes", C.c_uint64),
+    ]
+
+
 class SysCfg(C.Structure):
     _fields_ = [
         ("sys_type", C.c_int32), ("protocol_type", C.c_int32), ("max_num_sharers", C.c_int32),
@@ -52,7 +59,7 @@ class SysCfg(C.Structure):
         ("num_levels", C.c_int32), ("num_cores", C.c_int32), ("freq", C.c_double),
         ("bus_latency", C.c_int32), ("page_miss_delay", C.c_int32),
         ("network", NetCfg), ("directory_cache", CacheCfg), ("tlb_cache", CacheCfg),
-        ("cache", CacheCfg * PU_MAX_LEVELS),
+        ("cache", CacheCfg * PU_MAX_LEVELS), ("dram", DramCfg),
     ]
 
 
@@ -77,6 +84,8 @@ class Stats(C.Structure):
         ("level", LevelStats * PU_MAX_LEVELS), ("directory", LevelStats), ("tlb", LevelStats),
         ("link_flits", C.c_uint64), ("mg1_calls", C.c_uint64), ("lockdown_calls", C.c_uint64),
         ("bus_accesses", C.c_uint64), ("requests", C.c_uint64), ("error_flags", C.c_uint64),
+        ("dram_row_hits", C.c_uint64), ("dram_row_empty", C.c_uint64), ("dram_row_conflicts", C.c_uint64),
+        ("dram_bank_wait", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -237,6 +237,20 @@ int parse_doc(const std::string& text, pu_sim_cfg* out) {
     cache_fields(d, tlb[0], &y.tlb_cache, &n);
     if (n != 6) return pu::set_error(PU_EINVAL, "Error in parsing TLB cache structure!");
 
+    // optional <dram> element (pu_dram_cfg: the opt-in bank model); the
+    // reference's XPath parser never looks at it
+    std::vector<int> dram = find_all(d, "dram");
+    if (dram.size() > 1) return pu::set_error(PU_EINVAL, "Error in parsing dram structure!");
+    if (dram.size() == 1) {
+        int m = 0;
+        field(d, dram[0], "banks", &y.dram.banks, &m);
+        field(d, dram[0], "row_bytes", &y.dram.row_bytes, &m);
+        field(d, dram[0], "t_rcd", &y.dram.t_rcd, &m);
+        field(d, dram[0], "t_rp", &y.dram.t_rp, &m);
+        field(d, dram[0], "t_burst", &y.dram.t_burst, &m);
+        if (m != 5) return pu::set_error(PU_EINVAL, "Error in parsing dram structure!");
+    }
+
     std::vector<int> caches = find_all(d, "cache");
     if ((int)caches.size() != y.num_levels) return pu::set_error(PU_EINVAL, "Error in parsing cache structure!");
     n = 0;
@@ -324,6 +338,15 @@ int pu_config_write_xml(const pu_sim_cfg* c, char* buf, size_t cap, size_t* writ
     for (int i = 0; i < y.num_levels && i < PU_MAX_LEVELS; i++) put_cache(o, i2, "cache", y.cache[i]);
     put_cache(o, i2, "directory_cache", y.directory_cache);
     put_cache(o, i2, "tlb_cache", y.tlb_cache);
+    if (y.dram.banks > 0) {   // the opt-in bank model only; reference configs stay config_prime's layout
+        o << i2 << "<dram>\n";
+        put(o, i3, "banks", y.dram.banks);
+        put(o, i3, "row_bytes", (long long)y.dram.row_bytes);
+        put(o, i3, "t_rcd", y.dram.t_rcd);
+        put(o, i3, "t_rp", y.dram.t_rp);
+        put(o, i3, "t_burst", y.dram.t_burst);
+        o << i2 << "</dram>\n";
+    }
     o << i1 << "</system>\n";
     o << "</simulator>\n";
     std::string s = o.str();

@@ -119,7 +119,7 @@ typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
 // adds with ds_add_u64 (no return, no wait) and the kernel flushes once.
 enum StatId {
     SN_ACC, SN_DIST, SN_TOTAL, SN_ROUTER, SN_LINK, SN_INJECT, SN_DRAM, SN_BUSCONT, SN_FLITS, SN_MG1,
-    SN_LOCKDOWN, SN_BUSACC, SN_REQS, SN_BCAST, SN_COUNT
+    SN_LOCKDOWN, SN_BUSACC, SN_REQS, SN_BCAST, SN_ROWHIT, SN_ROWEMPTY, SN_ROWCONF, SN_BANKWAIT, SN_COUNT
 };
 static __shared__ unsigned long long lds_stat[SN_COUNT];
 static __shared__ unsigned long long lds_err;
@@ -999,9 +999,36 @@ struct Engine {
         if (ln == 0) atomic_add_u64(at<uint64_t>(off_cnt) + (size_t)cid * 4 + which, 1ull);
     }
 
-    __device__ __forceinline__ int dram() {
+    // Dram::access (dram.cpp:43-47) at cycle t for line address addr: the
+    // reference's fixed latency, or with the opt-in bank model (Geo.dram_banks
+    // > 0, pu_dram_cfg; no reference counterpart) one open-page bank access.
+    // The bank record is read by every lane (one broadcast line) and written
+    // by lane 0; its delay only depends on wave-uniform values.
+    __device__ __forceinline__ int dram(uint64_t addr, int64_t t) {
         stat_add(SN_DRAM, 1);
-        return g->dram_access_time;
+        if (g->dram_banks == 0) return g->dram_access_time;
+        const uint64_t row = uni64(addr) >> g->dram_row_shift;
+        const uint64_t bank = row & (uint64_t)(g->dram_banks - 1);
+        const uint64_t page = (row >> g->dram_bank_shift) + 1;   // + 1: 0 means closed
+        t = (int64_t)uni64((uint64_t)t);
+        DramBank* B = at<DramBank>(g->off_dram) + bank;
+        const int64_t ready = (int64_t)uni64((uint64_t)B->ready);
+        const uint64_t open = uni64(B->open);
+        const int64_t start = ready > t ? ready : t;
+        int64_t act;
+        if (open == page) {
+            act = 0;
+            stat_add(SN_ROWHIT, 1);
+        } else if (open == 0) {
+            act = g->dram_t_rcd;
+            stat_add(SN_ROWEMPTY, 1);
+        } else {
+            act = (int64_t)g->dram_t_rp + g->dram_t_rcd;
+            stat_add(SN_ROWCONF, 1);
+        }
+        if (ln == 0) *B = DramBank{start + act + g->dram_t_burst, page};
+        stat_add(SN_BANKWAIT, (uint64_t)(start - t));
+        return (int)(start - t + act) + g->dram_access_time;
     }
 
     // ------------------------------------------------------------ downward propagation
@@ -1358,10 +1385,10 @@ struct Engine {
                     pinval = false;                  // share, not inval (system.cpp:660-671)
                     st = ST_S;
                 } else if (st == ST_S) {
-                    if (!shared) delay += dram();
+                    if (!shared) delay += dram(r.addr, timer + delay);
                     if (g->protocol_type == 1 && count_sharers(nsh, sh) >= g->max_num_sharers) st = ST_B;
                 } else if (st == ST_B) {
-                    if (!shared) delay += dram();
+                    if (!shared) delay += dram(r.addr, timer + delay);
                 } else if (st == ST_V) {
                     st = ST_E;
                 }
@@ -1370,7 +1397,7 @@ struct Engine {
                 pool_release(nsh, sh);
                 nsh = 0;
                 sh = 0;
-                dram();
+                dram(r.addr, timer + delay);
             }
         }
         if (pmode != PR_NONE) {
@@ -1379,13 +1406,13 @@ struct Engine {
             psh = sh;
             delay = probe(pmode, pone, psh_n, psh, pinval, preply, home, pr, timer, delay);
         }
-        if (extra_dram == 1) dram();
-        if (extra_dram == 2) delay += dram();
+        if (extra_dram == 1) dram(pr.addr, timer + delay);   // the evicted owner's write-back
+        if (extra_dram == 2) delay += dram(r.addr, timer + delay);
         if (release_set) {                   // sharer_set.clear(); insert(cache_id)
             pool_release(nsh, sh);
             nsh = 1;
             sh = (uint64_t)cid;
-            if (miss_fill) delay += dram();
+            if (miss_fill) delay += dram(r.addr, timer + delay);
 
         } else if (r.type == PU_RD) {
             add_sharer(nsh, sh, cid);
@@ -1652,7 +1679,7 @@ struct Engine {
             if (is_miss) {
                 ret = r.type == PU_WR ? ST_M : (shared_line ? ST_S : ST_E);
                 set_state(v, meta, way, ret);
-                dly += dram();
+                dly += dram(r.addr, timer + dly);
             } else {
                 set_state(v, meta, way, ST_M);
             }
@@ -1773,6 +1800,10 @@ struct Engine {
         atomic_add_u64(&S->lockdown_calls, lds_stat[SN_LOCKDOWN]);
         atomic_add_u64(&S->bus_accesses, lds_stat[SN_BUSACC]);
         atomic_add_u64(&S->requests, lds_stat[SN_REQS]);
+        atomic_add_u64(&S->dram_row_hits, lds_stat[SN_ROWHIT]);
+        atomic_add_u64(&S->dram_row_empty, lds_stat[SN_ROWEMPTY]);
+        atomic_add_u64(&S->dram_row_conflicts, lds_stat[SN_ROWCONF]);
+        atomic_add_u64(&S->dram_bank_wait, lds_stat[SN_BANKWAIT]);
         __hip_atomic_fetch_or(&S->error_flags, (uint64_t)lds_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 };

@@ -23,6 +23,7 @@
 //            interval start, so the M/G/1-vs-tree decision of a hop needs the
 //            header only)  — links first, then per-cache buses
 //     qring: nqueues x 128 x {first,second} (2 KB)
+//   dram : banks x DramBank (opt-in bank model, pu_dram_cfg; absent when off)
 //   stats (EngineStats), per-core completion cycles, run state.
 //
 // Lane ownership inside the wavefront that runs a replica: way w of any set
@@ -101,7 +102,15 @@ struct EngineStats {
         net_inject_delay, dram_accesses, total_bus_contention;
     int64_t total_num_broadcast;
     uint64_t link_flits, mg1_calls, lockdown_calls, bus_accesses, requests, error_flags;
-    uint64_t _pad;
+    uint64_t dram_row_hits, dram_row_empty, dram_row_conflicts, dram_bank_wait;
+};
+
+// One DRAM bank of the opt-in bank model (pu_dram_cfg): the cycle it is free
+// again and its open page + 1 (0 = closed).  Zeroed at reset: every bank
+// closed and free from cycle 0.
+struct DramBank {
+    int64_t ready;
+    uint64_t open;
 };
 
 struct LevelGeo {
@@ -157,6 +166,10 @@ struct Geo {
     TlbGeo tlb;
     uint64_t off_qhdr, off_qring, off_stats, off_completion, off_run;
     uint64_t off_core_shift;        // closed-loop replay: int64 per core (sum of its batch delays)
+    // DRAM bank model (dram_banks = 0: the reference's fixed latency)
+    int32_t dram_banks, dram_bank_shift, dram_row_shift, dram_t_rcd;
+    int32_t dram_t_rp, dram_t_burst;
+    uint64_t off_dram;              // dram_banks x DramBank
     uint64_t replica_bytes;
 };
 

@@ -196,6 +196,22 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
     }
     for (int l = 0; l < y.num_levels; l++)
         if (g->lv[l].has_bus) g->lv[l].bus_q0 += g->nlinks;
+    const pu_dram_cfg& dm = y.dram;   // opt-in bank model (pu_dram_cfg); 0 banks = the reference's Dram
+    if (dm.banks < 0 || dm.banks > (1 << 20) || (dm.banks & (dm.banks - 1)) != 0)
+        return pu::set_error(PU_EINVAL, "dram banks must be 0 or a power of two <= 2^20");
+    if (dm.banks > 0) {
+        if (dm.row_bytes < 64 || (dm.row_bytes & (dm.row_bytes - 1)) != 0 || dm.row_bytes > (1ull << 40))
+            return pu::set_error(PU_EINVAL, "dram row_bytes must be a power of two in [64, 2^40]");
+        if (dm.t_rcd < 0 || dm.t_rp < 0 || dm.t_burst < 0 || dm.t_rcd >= (1 << 24) || dm.t_rp >= (1 << 24) ||
+            dm.t_burst >= (1 << 24))
+            return pu::set_error(PU_EINVAL, "dram timings must be in [0, 2^24) cycles");
+        g->dram_banks = dm.banks;
+        g->dram_bank_shift = ilog2((uint64_t)dm.banks);
+        g->dram_row_shift = ilog2(dm.row_bytes);
+        g->dram_t_rcd = dm.t_rcd;
+        g->dram_t_rp = dm.t_rp;
+        g->dram_t_burst = dm.t_burst;
+    }
 
     // ---- layout
     for (int l = 0; l < y.num_levels; l++) {
@@ -243,6 +259,7 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
     g->off_completion = lay.take((uint64_t)y.num_cores * 8);
     g->off_run = lay.take(sizeof(RunState));
     g->off_core_shift = lay.take((uint64_t)y.num_cores * 8);
+    g->off_dram = lay.take((uint64_t)g->dram_banks * sizeof(DramBank));
     g->replica_bytes = align_up(lay.cur, 4096);
     return 0;
 }
@@ -784,6 +801,10 @@ int pu_stats_get(pu_handle* h, int replica, pu_stats* out) {
     out->bus_accesses = es.bus_accesses;
     out->requests = es.requests;
     out->error_flags = es.error_flags;
+    out->dram_row_hits = es.dram_row_hits;
+    out->dram_row_empty = es.dram_row_empty;
+    out->dram_row_conflicts = es.dram_row_conflicts;
+    out->dram_bank_wait = es.dram_bank_wait;
     return 0;
 }
 
@@ -829,6 +850,13 @@ long pu_report(pu_handle* h, int replica, int include_time, char* buf, size_t ca
     // Dram::report
     o << "DRAM Statistics:\n";
     o << "Total # of DRAM accesses: " << es.dram_accesses << std::endl;
+    if (g.dram_banks > 0) {   // opt-in bank model (pu_dram_cfg): lines the reference never prints
+        o << "DRAM banks: " << g.dram_banks << ", row bytes: " << y.dram.row_bytes << std::endl;
+        o << "Row buffer hits: " << es.dram_row_hits << std::endl;
+        o << "Row buffer misses (bank closed): " << es.dram_row_empty << std::endl;
+        o << "Row buffer conflicts: " << es.dram_row_conflicts << std::endl;
+        o << "Total bank wait cycles: " << es.dram_bank_wait << std::endl;
+    }
     o << std::endl << "Simulation result for cache system: \n\n";
     if (y.verbose_report) {
         o << "Home Occupation:\n";

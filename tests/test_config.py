@@ -1,4 +1,5 @@
 """config_prime XML schema loader vs the reference's XmlParser (xml_parser.cpp)."""
+import ctypes as C
 import json
 import os
 
@@ -11,9 +12,10 @@ from golden_util import GOLDEN, case_names
 
 
 def _as_dict(cfg):
+    """The XmlSim fields (pu_sys_cfg.dram, the opt-in bank model, has no XmlSys counterpart)."""
     def conv(o):
         if isinstance(o, (A.CacheCfg, A.NetCfg, A.SysCfg, A.SimCfg)):
-            return {k: conv(getattr(o, k)) for k, _ in o._fields_ if not k.startswith("_")}
+            return {k: conv(getattr(o, k)) for k, _ in o._fields_ if not k.startswith("_") and k != "dram"}
         if hasattr(o, "__len__") and not isinstance(o, (str, bytes)):
             return [conv(x) for x in o]
         return o
@@ -93,3 +95,21 @@ def test_write_xml_round_trip():
     assert P.uncore.lib().pu_config_write_xml(C.byref(cfg), buf, len(buf), C.byref(n)) == 0
     again = P.parse_config(buf.value.decode())
     assert _as_dict(again) == _as_dict(cfg)
+
+
+def test_dram_bank_element_round_trip():
+    """The optional <dram> element (pu_dram_cfg) parses, is written back only
+    when banks > 0, and malformed or partial elements are refused."""
+    sim = CF.default_config()
+    assert P.config_from_dict(sim).sys.dram.banks == 0
+    sim["system"]["dram"] = {"banks": 16, "row_bytes": 8192, "t_rcd": 14, "t_rp": 14, "t_burst": 4}
+    cfg = P.config_from_dict(sim)
+    d = cfg.sys.dram
+    assert (d.banks, d.row_bytes, d.t_rcd, d.t_rp, d.t_burst) == (16, 8192, 14, 14, 4)
+    buf, n = C.create_string_buffer(1 << 16), C.c_size_t(0)
+    assert P.uncore.lib().pu_config_write_xml(C.byref(cfg), buf, len(buf), C.byref(n)) == 0
+    text = buf.value.decode()
+    assert "<dram>" in text and P.parse_config(text).sys.dram.row_bytes == 8192
+    del sim["system"]["dram"]["t_rp"]
+    with pytest.raises(P.UncoreError):
+        P.config_from_dict(sim)
