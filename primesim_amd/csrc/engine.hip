@@ -208,20 +208,41 @@ __device__ __forceinline__ void ring_load(const NetCtx& c, int q, uint32_t head,
     asm volatile("" : "+v"(v.lf), "+v"(v.ls), "+v"(v.hf), "+v"(v.hs));
 }
 
+// IEEE double division a / b, correctly rounded, as hipcc's own lowering does
+// it (v_rcp_f64, two Newton steps, one residual correction) minus its
+// range-scaling and special-case steps (v_div_scale/v_div_fixup): every
+// M/G/1 operand is a positive normal double far from overflow and underflow
+// (counts, cycle sums and their ratios), where those steps are the identity,
+// so the result is the same correctly rounded quotient.  The refined
+// reciprocal of a shared divisor is computed once.
+__device__ __forceinline__ double rcp_nr(double b) {
+    double y = __builtin_amdgcn_rcp(b);
+    y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+    return __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+}
+__device__ __forceinline__ double div_nr(double a, double b, double y) {
+    const double q = a * y;
+    return __builtin_fma(__builtin_fma(-b, q, a), y, q);
+}
+
 // M/G/1 (queue_model_m_g_1.cpp:16-42), reference operation order.
 __device__ __forceinline__ uint64_t mg1_wait(const QState& s) {
     if (s.n == 0) return 0;
     double nd = (double)s.n;
-    double mean = s.sum / nd;
-    double var = (s.sum_sq / nd) - mean * mean;
-    double mu = 1.0 / mean;
-    double lambda = nd / (double)s.newest;
+    const double rn = rcp_nr(nd);
+    double mean = div_nr(s.sum, nd, rn);
+    double var = div_nr(s.sum_sq, nd, rn) - mean * mean;
+    double mu = div_nr(1.0, mean, rcp_nr(mean));
+    const double newest = (double)s.newest;
+    double lambda = div_nr(nd, newest, rcp_nr(newest));
     if (lambda >= mu) lambda = 0.999 * mu;
-    double inv = 1.0 / (mu * mu);
+    const double mu2 = mu * mu;
+    double inv = div_nr(1.0, mu2, rcp_nr(mu2));
     double num = 0.5 * mu;
     num = num * lambda;
     num = num * (inv + var);
-    double w = num / (mu - lambda);
+    const double den = mu - lambda;
+    double w = div_nr(num, den, rcp_nr(den));
     return (uint64_t)ceil(w);
 }
 
@@ -574,45 +595,27 @@ __device__ __forceinline__ void net_coords(const NetCtx& c, int id, int& x, int&
         z = 0;
     }
 }
-// Network::getLink (network.cpp:213-307): one record per undirected edge.
-__device__ __forceinline__ int net_link(const NetCtx& c, int x, int y, int z, int dir) {
-    const int w = c.w;
-    int a, b, cc;
-    if (c.net_type == 1) {
-        switch (dir) {
-            case 0: a = x; b = y; cc = z; break;
-            case 1: a = x - 1; b = y; cc = z; break;
-            case 2: a = y - 1; b = z; cc = x + w; break;
-            case 3: a = y; b = z; cc = x + w; break;
-            case 4: a = z; b = x; cc = y + 2 * w; break;
-            default: a = z - 1; b = x; cc = y + 2 * w; break;
-        }
-        return (a * w + b) * (3 * w) + cc;
-    }
-    switch (dir) {
-        case 0: a = x; b = y; break;
-        case 1: a = x - 1; b = y; break;
-        case 2: a = y - 1; b = x + w; break;
-        default: a = y; b = x + w; break;
-    }
-    return a * (2 * w) + b;
-}
-// link of hop h of the X-then-Y-then-Z route from (sx,sy,sz) to (rx,ry,rz)
+// Network::getLink (network.cpp:213-307), one record per undirected edge: the
+// link of hop h of the X-then-Y-then-Z route from (sx,sy,sz) to (rx,ry,rz),
+// computed branch-free across lanes (hops of one route take different ranges):
+// hop h < hx moves along x at (sy, sz), then along y at (rx, sz), then along z
+// at (rx, ry); a = the coordinate (or coordinate - 1 moving down), and the link
+// id is net_link's (network.cpp:213-307): 2-D a*(2w) + b with b = sy | rx + w,
+// 3-D (a*w + b)*(3w) + cc with (b, cc) = (sy, sz) | (sz, rx + w) | (rx, ry + 2w).
 __device__ __forceinline__ int net_route_link(const NetCtx& c, int h, int sx, int sy, int sz, int rx, int ry, int rz,
                                               int hx, int hy) {
-    if (h < hx) {
-        int e = rx > sx;
-        int x = e ? sx + h : sx - h;
-        return net_link(c, x, sy, sz, e ? 0 : 1);
-    }
-    if (h < hx + hy) {
-        int s = ry > sy;
-        int y = s ? sy + (h - hx) : sy - (h - hx);
-        return net_link(c, rx, y, sz, s ? 3 : 2);
-    }
-    int u = rz > sz;
-    int z = u ? sz + (h - hx - hy) : sz - (h - hx - hy);
-    return net_link(c, rx, ry, z, u ? 4 : 5);
+    const int w = c.w;
+    const bool e = rx > sx, n = ry > sy, u = rz > sz;   // wave-uniform
+    const bool inx = h < hx, iny = h < hx + hy;
+    const int hy_ = h - hx, hz_ = h - hx - hy;
+    const int ax = e ? sx + h : sx - h - 1;
+    const int ay = n ? sy + hy_ : sy - hy_ - 1;
+    if (c.net_type != 1) return inx ? ax * (2 * w) + sy : ay * (2 * w) + rx + w;
+    const int az = u ? sz + hz_ : sz - hz_ - 1;
+    const int A = inx ? ax : iny ? ay : az;
+    const int B = inx ? sy : iny ? sz : rx;
+    const int CC = inx ? sz : iny ? rx + w : ry + 2 * w;
+    return (A * w + B) * (3 * w) + CC;
 }
 
 // LDS staging ring for predicted tree hops: PU_RING_PF full link rings per wave
