@@ -130,6 +130,13 @@ def reference_engine(cfg_xml: str, cfg, mode: int = 0):
     return kind, eng
 
 
+def simulated(n: int, rc: int) -> int:
+    """Requests of one reference run() call that were actually simulated: all
+    of them (rc 0), the first rc (the prime.cpp:130-134 stop after request
+    rc-1), or none (rc -1: already stopped)."""
+    return n if rc == 0 else max(rc, 0)
+
+
 def cpu_baseline(cfg_xml: str, cfg, reqs: np.ndarray, threads, fill: int, budget_s: float, mode: int = 0):
     """Time the reference CPU uncore (or the restatement) on reqs[fill:], after
     an untimed run over reqs[:fill]; returns every delay it produced."""
@@ -141,14 +148,17 @@ def cpu_baseline(cfg_xml: str, cfg, reqs: np.ndarray, threads, fill: int, budget
     for a in range(0, fill, chunk):
         d, rc = eng.run(reqs[a:min(fill, a + chunk)])
         delays.append(d)
-    done = fill
+    done, sim = fill, 0
     t0 = time.perf_counter()
     while done < len(reqs) and time.perf_counter() - t0 < budget_s:
         d, rc = eng.run(reqs[done:done + chunk])
         delays.append(d)
         done += len(d)
+        sim += simulated(len(d), rc)
+        if rc != 0:                                   # prime.cpp:130-134 stop: nothing more is simulated
+            break
     el = time.perf_counter() - t0
-    return kind, done - fill, el, np.concatenate(delays) if delays else np.zeros(0, np.int32)
+    return kind, sim, el, np.concatenate(delays) if delays else np.zeros(0, np.int32)
 
 
 # ---------------------------------------------------------------- CPU ensemble
@@ -166,11 +176,14 @@ def _ensemble_worker(conn, cfg_xml: str, seed: int, fill: int, n_timed: int, bud
             eng.run(reqs[a:min(fill, a + 16384)])
         conn.send(("ready", kind))
         conn.recv()                                   # go
-        done, t0 = fill, time.perf_counter()
+        done, sim, t0 = fill, 0, time.perf_counter()
         while done < len(reqs) and time.perf_counter() - t0 < budget_s:
-            d, _ = eng.run(reqs[done:done + 2048])
+            d, rc = eng.run(reqs[done:done + 2048])
             done += len(d)
-        conn.send(("done", done - fill, time.perf_counter() - t0))
+            sim += simulated(len(d), rc)
+            if rc != 0:                               # halted: the rest would only be skipped
+                break
+        conn.send(("done", sim, time.perf_counter() - t0))
     except Exception as e:  # noqa: BLE001 — reported to the parent
         conn.send(("error", repr(e)))
     finally:
@@ -558,7 +571,7 @@ def main() -> None:
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": "uncore_kernel<1, true>",
+                "kernel": "uncore_kernel<1, true, false>",
                 "avg_launch_ms": avg_ms,
                 "alg_bytes_per_launch": bytes_per_launch,
                 "limiter": "instruction issue and dependent-load latency (profiles/r2_*sq*), not HBM bandwidth",

@@ -29,7 +29,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "uncore_kernel<1, true>"   # the timed (time-sliced) launches of bench.py
+KERNEL = "uncore_kernel<1, true, false>"   # the timed (time-sliced, headers in HBM) launches of bench.py
 
 
 def run(cmd, log):
