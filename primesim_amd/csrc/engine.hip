@@ -92,7 +92,7 @@ struct RingView {
 // A queue header (QueueHdr dwords 0-13) as held by a lane.
 struct QState {
     uint32_t head, count;
-    uint64_t n;
+    double n;           // _num_arrivals, held as an exact double (< 2^53)
     double sum, sum_sq;
     uint64_t newest;
     uint64_t f0;
@@ -106,9 +106,10 @@ struct QState {
 // 128 VGPRs).  The one-level engine fits 128 with a 4-VGPR spill and runs 7%
 // faster at 4 resident waves than at 3 (150 VGPRs); the deeper hierarchies
 // would spill ~120 VGPRs at 128, so they keep the compiler's choice.
-#ifndef PU_MIN_WAVES
-#define PU_MIN_WAVES(NL) ((NL) == 1 ? 4 : 1)
+#ifndef PU_WAVES_1LEVEL
+#define PU_WAVES_1LEVEL 4
 #endif
+#define PU_MIN_WAVES(NL) ((NL) == 1 ? PU_WAVES_1LEVEL : 1)
 // native vectors (not classes), so loads/stores through global-address-space
 // pointers need no conversion: slot = {first, second}, header = 10 dwords
 typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
@@ -134,6 +135,16 @@ struct LoopCtl {
     uint32_t flags, _pad;
 };
 static __shared__ LoopCtl lds_ctl;
+// Engine state that only the sharer pool and the page table touch: in LDS, so
+// it holds no scalar registers across the request loop (every lane reads and
+// writes the same wave-uniform value).
+struct EngShared {
+    int32_t pool_top;    // sharer-bitmap pool stack (RunState.pool_top)
+    int32_t stop;        // replica must stop (engine limit)
+    uint64_t page_next;  // RunState.page_next
+    uint64_t last_addr;  // RunState.last_addr
+};
+static __shared__ EngShared lds_eng;
 
 __device__ __forceinline__ void stat_add(int k, uint64_t v) {
     if (lane_id() == 0) atomicAdd(&lds_stat[k], (unsigned long long)v);
@@ -227,8 +238,8 @@ __device__ __forceinline__ double div_nr(double a, double b, double y) {
 
 // M/G/1 (queue_model_m_g_1.cpp:16-42), reference operation order.
 __device__ __forceinline__ uint64_t mg1_wait(const QState& s) {
-    if (s.n == 0) return 0;
-    double nd = (double)s.n;
+    if (s.n == 0.0) return 0;
+    const double nd = s.n;
     const double rn = rcp_nr(nd);
     double mean = div_nr(s.sum, nd, rn);
     double var = div_nr(s.sum_sq, nd, rn) - mean * mean;
@@ -488,7 +499,8 @@ __device__ __forceinline__ uint32_t* hdr_ptr(const NetCtx& c, int q) {
 template <bool LH>
 __device__ __forceinline__ void q_store_hdr(const NetCtx& c, int q, const QState& st) {
     uint64_t sb = (uint64_t)__double_as_longlong(st.sum), qb = (uint64_t)__double_as_longlong(st.sum_sq);
-    const v4u32 a = v4u32{st.head, st.count, (uint32_t)st.n, (uint32_t)(st.n >> 32)};
+    const uint64_t nb = (uint64_t)__double_as_longlong(st.n);
+    const v4u32 a = v4u32{st.head, st.count, (uint32_t)nb, (uint32_t)(nb >> 32)};
     const v4u32 b = v4u32{(uint32_t)sb, (uint32_t)(sb >> 32), (uint32_t)qb, (uint32_t)(qb >> 32)};
     const v4u32 cc = v4u32{(uint32_t)st.newest, (uint32_t)(st.newest >> 32), (uint32_t)st.f0, (uint32_t)(st.f0 >> 32)};
     if constexpr (LH) {
@@ -509,7 +521,7 @@ template <bool LH>
 __device__ __forceinline__ void q_finish(const NetCtx& c, int q, QState& st, uint64_t t, uint64_t p, uint64_t d) {
     st.sum_sq = st.sum_sq + (double)p * (double)p;
     st.sum = st.sum + (double)p;
-    st.n = st.n + 1;
+    st.n = st.n + 1.0;
     uint64_t fin = t + d + p;
     st.newest = fin > st.newest ? fin : st.newest;
     if (lane_id() == 0) q_store_hdr<LH>(c, q, st);
@@ -543,7 +555,7 @@ __device__ __forceinline__ QState hdr_state(v4u32 a, v4u32 b, v4u32 c) {
     QState st;
     st.head = a.x;
     st.count = a.y;
-    st.n = u64of(a.z, a.w);
+    st.n = __longlong_as_double((long long)u64of(a.z, a.w));
     st.sum = __longlong_as_double((long long)u64of(b.x, b.y));
     st.sum_sq = __longlong_as_double((long long)u64of(b.z, b.w));
     st.newest = u64of(c.x, c.y);
@@ -856,7 +868,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
             st.f0 = vf0;
             st.sum_sq = st.sum_sq + (double)plen * (double)plen;
             st.sum = st.sum + (double)plen;
-            st.n = st.n + 1;
+            st.n = st.n + 1.0;
             st.newest = vfin > st.newest ? vfin : st.newest;
             q_store_hdr<LH>(c, rq, st);
         }
@@ -895,10 +907,13 @@ struct Engine {
     // reference System scratch for the requesting core (delay[core], hit_flag[core])
     int dly;
     bool hit;
-    int32_t pool_top;    // sharer-bitmap pool stack (RunState.pool_top)
-    bool stop;           // replica must stop (pool exhausted)
-    uint64_t page_next;  // RunState.page_next
-    uint64_t last_addr;  // RunState.last_addr
+
+    __device__ __forceinline__ void init_shared(int32_t pool_top, uint64_t page_next, uint64_t last_addr) const {
+        lds_eng.pool_top = pool_top;
+        lds_eng.stop = 0;
+        lds_eng.page_next = page_next;
+        lds_eng.last_addr = last_addr;
+    }
 
 
     template <class T>
@@ -1112,17 +1127,19 @@ struct Engine {
     }
     __device__ __forceinline__ void pool_release(uint32_t nsh, uint64_t sh) {
         if (nsh != PU_SH_POOL) return;
-        if (ln == 0) at<int32_t>(g->dir.off_pool_free)[pool_top] = (int32_t)sh;
-        pool_top++;
+        const int32_t pt = (int32_t)uni32((uint32_t)lds_eng.pool_top);
+        if (ln == 0) at<int32_t>(g->dir.off_pool_free)[pt] = (int32_t)sh;
+        lds_eng.pool_top = pt + 1;
     }
     __device__ __forceinline__ bool pool_alloc(uint64_t* idx) {
-        if (pool_top <= 0) {
+        const int32_t pt = (int32_t)uni32((uint32_t)lds_eng.pool_top);
+        if (pt <= 0) {
             err_or(PU_ERRF_POOL);
-            stop = true;
+            lds_eng.stop = 1;
             return false;
         }
-        pool_top--;
-        uint32_t v = ln == 0 ? (uint32_t)at<int32_t>(g->dir.off_pool_free)[pool_top] : 0u;
+        lds_eng.pool_top = pt - 1;
+        uint32_t v = ln == 0 ? (uint32_t)at<int32_t>(g->dir.off_pool_free)[pt - 1] : 0u;
         *idx = rl32(v, 0);
         return true;
     }
@@ -1719,18 +1736,19 @@ struct Engine {
             const int fe = me ? (int)__builtin_ctzll(me) : 64;
             if (mm && (int)__builtin_ctzll(mm) < fe) return rl64(e.ppage, (int)__builtin_ctzll(mm));
             if (me) {
-                if (page_next * 4 >= T.pages_cap * 3) {       // keep probes short; engine limit
+                const uint64_t pp = uni64(lds_eng.page_next);
+                if (pp * 4 >= T.pages_cap * 3) {              // keep probes short; engine limit
                     err_or(PU_ERRF_PAGES);
-                    stop = true;
+                    lds_eng.stop = 1;
                 }
-                const uint64_t pp = page_next++;
+                lds_eng.page_next = pp + 1;
                 if (ln == fe) tab[slot] = PageEnt{vpage, prog, 1u, pp, 0ull};
                 return pp;
             }
             h = (h + 64) & mask;
         }
         err_or(PU_ERRF_PAGES);
-        stop = true;
+        lds_eng.stop = 1;
         return 0;
     }
 
@@ -1779,7 +1797,7 @@ struct Engine {
         Req r = r_in;
         if (g->tlb_enable) {
             dly = tlb_translate(core, r, timer);
-            last_addr = r.addr;
+            lds_eng.last_addr = r.addr;
         }
         if (g->sys_type == 0) mesi<0>(core, r, timer + dly);
         else mesi_bus<0>(core, r, timer + dly);
@@ -1879,10 +1897,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
         lds_ctl.done = 0;
     }
     __builtin_amdgcn_wave_barrier();
-    e.pool_top = (int32_t)rl32(e.ln == 0 ? (uint32_t)rs->pool_top : 0u, 0);
-    e.page_next = rl64(e.ln == 0 ? rs->page_next : 0ull, 0);
-    e.last_addr = rl64(e.ln == 0 ? rs->last_addr : 0ull, 0);
-    e.stop = false;
+    e.init_shared((int32_t)rl32(e.ln == 0 ? (uint32_t)rs->pool_top : 0u, 0), rl64(e.ln == 0 ? rs->page_next : 0ull, 0),
+                  rl64(e.ln == 0 ? rs->last_addr : 0ull, 0));
     const uint64_t b = pos ? pos[blockIdx.x] : off[blockIdx.x], end = off[blockIdx.x + 1];
     uint64_t i = b;
     for (; i < end; i++) {
@@ -1930,7 +1946,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
                     lds_ctl.halted = 1;
                 }
             }
-            if (e.stop) {                        // engine limit hit: cannot continue exactly
+            if (lds_eng.stop) {                  // engine limit hit: cannot continue exactly
                 lds_ctl.halted = 1;
                 lds_ctl.skip = 0;
             }
@@ -1953,9 +1969,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
         rs->msg_shift = lds_ctl.msg_shift;
         rs->dead_tags = lds_ctl.dead_tags;
         rs->processed += lds_ctl.done;
-        rs->pool_top = e.pool_top;
-        rs->page_next = e.page_next;
-        rs->last_addr = e.last_addr;
+        rs->pool_top = lds_eng.pool_top;
+        rs->page_next = lds_eng.page_next;
+        rs->last_addr = lds_eng.last_addr;
     }
     __syncthreads();
     e.flush_stats();
@@ -2000,10 +2016,7 @@ __global__ __launch_bounds__(64) void unit_queue_kernel(const Geo* __restrict__ 
     e.g = g;
     e.ln = lane_id();
     e.base = base;
-    e.pool_top = 0;
-    e.stop = false;
-    e.page_next = 0;
-    e.last_addr = 0;
+    e.init_shared(0, 0, 0);
     const NetCtx c = e.net_ctx();
     uint64_t calls = 0, err = 0;
     for (uint64_t i = 0; i < n; i++) {
@@ -2024,10 +2037,7 @@ __global__ __launch_bounds__(64) void unit_network_kernel(const Geo* __restrict_
     e.ln = lane_id();
     e.base = base;
     stats_init();
-    e.pool_top = 0;
-    e.stop = false;
-    e.page_next = 0;
-    e.last_addr = 0;
+    e.init_shared(0, 0, 0);
     for (uint64_t i = 0; i < n; i++) {
         uint64_t d = e.transmit(src[i], dst[i], len[i], timer[i]);
         if (e.ln == 0) out[i] = d;

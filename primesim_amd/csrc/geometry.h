@@ -84,7 +84,7 @@ struct DirLine {
 struct QueueHdr {
     uint32_t head;
     uint32_t count;
-    uint64_t n;        // QueueModelMG1::_num_arrivals
+    double n;          // QueueModelMG1::_num_arrivals as an exact double (< 2^53; 0.0 is all-zero bits)
     double sum;        // _sigma_service_time
     double sum_sq;     // _sigma_service_time_square
     uint64_t newest;   // _newest_arrival_time
