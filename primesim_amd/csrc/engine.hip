@@ -100,14 +100,15 @@ struct QState {
 
 #define AS1 __attribute__((address_space(1)))
 #ifndef PU_RING_PF
-#define PU_RING_PF 4   // staged rings in flight per wave (8 KB LDS)
+#define PU_RING_PF 3   // staged rings in flight per wave (6 KB LDS: 5 waves/SIMD fit the CU's 160 KB)
 #endif
-// Waves per SIMD the kernel is compiled for (the register budget: 4 waves =
-// 128 VGPRs).  The one-level engine fits 128 with a 4-VGPR spill and runs 7%
-// faster at 4 resident waves than at 3 (150 VGPRs); the deeper hierarchies
+// Waves per SIMD the kernel is compiled for (the register budget: 5 waves =
+// 96 VGPRs).  The one-level engine fits 96 with a 5-VGPR spill (once the
+// pool/page-table state moved to LDS) and runs 2.9% faster at 5 resident
+// waves than at 4 (120 VGPRs, no spill; same-box A/B); the deeper hierarchies
 // would spill ~120 VGPRs at 128, so they keep the compiler's choice.
 #ifndef PU_WAVES_1LEVEL
-#define PU_WAVES_1LEVEL 4
+#define PU_WAVES_1LEVEL 5
 #endif
 #define PU_MIN_WAVES(NL) ((NL) == 1 ? PU_WAVES_1LEVEL : 1)
 // native vectors (not classes), so loads/stores through global-address-space
