@@ -118,11 +118,15 @@ typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
 
 // Per-wave statistics in LDS (one workgroup = one wave = one replica); lane 0
-// adds with ds_add_u64 (no return, no wait) and the kernel flushes once.
+// adds with ds_add_u64 (no return, no wait) and the kernel flushes once.  A
+// transmit adds its six network sums at once (lanes 0-5); the router, link and
+// inject delay totals are derived from them at the flush (Network::transmit's
+// per-packet terms are linear in them, network.cpp:146-156).
 enum StatId {
-    SN_ACC, SN_DIST, SN_TOTAL, SN_ROUTER, SN_LINK, SN_INJECT, SN_DRAM, SN_BUSCONT, SN_FLITS, SN_MG1,
+    SN_ACC, SN_DIST, SN_TOTAL, SN_PLEN, SN_FLITS, SN_MG1, SN_DRAM, SN_BUSCONT,
     SN_LOCKDOWN, SN_BUSACC, SN_REQS, SN_BCAST, SN_ROWHIT, SN_ROWEMPTY, SN_ROWCONF, SN_BANKWAIT, SN_COUNT
 };
+constexpr uint32_t SN_NET_LANES = 0x3F;   // SN_ACC .. SN_MG1
 static __shared__ unsigned long long lds_stat[SN_COUNT];
 static __shared__ unsigned long long lds_err;
 // The message loop's state (uncore_kernel), lane 0 its writer.
@@ -147,11 +151,55 @@ struct EngShared {
 };
 static __shared__ EngShared lds_eng;
 
+// LDS updates by a fixed set of lanes, with the exec mask narrowed inside
+// the asm: written as `if (lane_id() == k)`, the lane compares are loop
+// invariants the compiler hoists and then spills (a v_readlane pair and a
+// wait state at every use).  LDS operations of a wave complete in order, so
+// the compiler's own lgkmcnt waits stay correct (at worst conservative).
+// s_and_b64 writes SCC, which the compiler may hold live across the asm: it
+// is declared clobbered.
+__device__ __forceinline__ void lds_add_u64_lanes(uint32_t lds_byte_addr, uint64_t v, uint32_t lanes) {
+    uint64_t keep;
+    asm volatile("s_mov_b64 %0, exec\n\t"
+                 "s_and_b64 exec, exec, %3\n\t"
+                 "ds_add_u64 %1, %2\n\t"
+                 "s_mov_b64 exec, %0"
+                 : "=&s"(keep) : "v"(lds_byte_addr), "v"(v), "s"((uint64_t)lanes) : "memory", "scc");
+}
+__device__ __forceinline__ void lds_or_u64_lane0(uint32_t lds_byte_addr, uint64_t v) {
+    uint64_t keep;
+    asm volatile("s_mov_b64 %0, exec\n\t"
+                 "s_and_b64 exec, exec, 1\n\t"
+                 "ds_or_b64 %1, %2\n\t"
+                 "s_mov_b64 exec, %0"
+                 : "=&s"(keep) : "v"(lds_byte_addr), "v"(v) : "memory", "scc");
+}
+// Device-scope atomic add by lane 0 (the per-cache counters), the same way.
+// Vector memory operations retire in issue order, so the compiler's vmcnt
+// waits (and vm_wait_dma's) stay correct with this one unseen: at worst they
+// wait for it too.
+__device__ __forceinline__ void gatomic_add_u64_lane0(uint64_t* p, uint64_t v) {
+    uint64_t keep;
+    asm volatile("s_mov_b64 %0, exec\n\t"
+                 "s_and_b64 exec, exec, 1\n\t"
+                 "global_atomic_add_x2 %1, %2, off\n\t"
+                 "s_mov_b64 exec, %0"
+                 : "=&s"(keep) : "v"(p), "v"(v) : "memory", "scc");
+}
+// lane L of v becomes the wave-uniform x (v_writelane_b32 with a constant lane)
+template <int L>
+__device__ __forceinline__ uint32_t wlane(uint32_t v, uint32_t x) {
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(uni32(x)), "i"(L));
+    return v;
+}
+__device__ __forceinline__ uint32_t lds_u32addr(const void* p) {
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
+}
 __device__ __forceinline__ void stat_add(int k, uint64_t v) {
-    if (lane_id() == 0) atomicAdd(&lds_stat[k], (unsigned long long)v);
+    lds_add_u64_lanes(lds_u32addr(&lds_stat[k]), v, 1u);
 }
 __device__ __forceinline__ void err_or(uint64_t f) {
-    if (lane_id() == 0) atomicOr(&lds_err, (unsigned long long)f);
+    lds_or_u64_lane0(lds_u32addr(&lds_err), f);
 }
 
 // Region cycle counters, compiled in only with -DPU_PROF (the profiling build,
@@ -883,17 +931,20 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
     t += c.router;
     t += (uint64_t)(plen - 1);
     const uint64_t dist = (uint64_t)hops;
-    {   // the eight network counters in one ds_add_u64, lane k adding counter k
-        const uint64_t tot = t - timer, rt = (dist + 1) * c.router;
-        uint64_t sv = ln == SN_ACC ? 1ull : 0ull;
-        sv = ln == SN_DIST ? dist : sv;
-        sv = ln == SN_TOTAL ? tot : sv;
-        sv = ln == SN_ROUTER ? rt : sv;
-        sv = ln == SN_LINK ? tot - rt - (uint64_t)(plen - 1) - c.inject : sv;
-        sv = ln == SN_INJECT ? c.inject : sv;
-        sv = ln == SN_FLITS ? dist * (uint64_t)plen : sv;
-        sv = ln == SN_MG1 ? mg1 : sv;
-        if (ln <= SN_MG1 && ln != SN_DRAM && ln != SN_BUSCONT) atomicAdd(&lds_stat[ln], (unsigned long long)sv);
+    {   // the six network sums in one ds_add_u64, lane k adding sum k (written
+        // into the lanes by v_writelane: no lane compares)
+        const uint64_t tot = t - timer, fl = dist * (uint64_t)plen;
+        uint32_t lo = 0, hi = 0;
+        lo = wlane<SN_ACC>(lo, 1u);
+        lo = wlane<SN_DIST>(lo, (uint32_t)dist);
+        lo = wlane<SN_TOTAL>(lo, (uint32_t)tot);
+        hi = wlane<SN_TOTAL>(hi, (uint32_t)(tot >> 32));
+        lo = wlane<SN_PLEN>(lo, (uint32_t)plen);
+        lo = wlane<SN_FLITS>(lo, (uint32_t)fl);
+        hi = wlane<SN_FLITS>(hi, (uint32_t)(fl >> 32));
+        lo = wlane<SN_MG1>(lo, (uint32_t)mg1);
+        hi = wlane<SN_MG1>(hi, (uint32_t)(mg1 >> 32));
+        lds_add_u64_lanes(lds_u32addr(&lds_stat[0]) + 8u * (uint32_t)ln, ((uint64_t)hi << 32) | lo, SN_NET_LANES);
     }
     if (err) err_or(err);
     return t - timer;
@@ -1015,7 +1066,7 @@ struct Engine {
         }
     }
     __device__ __forceinline__ void count(uint64_t off_cnt, int cid, int which) const {
-        if (ln == 0) atomic_add_u64(at<uint64_t>(off_cnt) + (size_t)cid * 4 + which, 1ull);
+        gatomic_add_u64_lane0(at<uint64_t>(off_cnt) + (size_t)cid * 4 + which, 1ull);
     }
 
     // Dram::access (dram.cpp:43-47) at cycle t for line address addr: the
@@ -1808,12 +1859,18 @@ struct Engine {
     __device__ void flush_stats() {
         if (ln != 0) return;
         EngineStats* S = at<EngineStats>(g->off_stats);
-        atomic_add_u64(&S->net_accesses, lds_stat[SN_ACC]);
-        atomic_add_u64(&S->net_distance, lds_stat[SN_DIST]);
-        atomic_add_u64(&S->net_total_delay, lds_stat[SN_TOTAL]);
-        atomic_add_u64(&S->net_router_delay, lds_stat[SN_ROUTER]);
-        atomic_add_u64(&S->net_link_delay, lds_stat[SN_LINK]);
-        atomic_add_u64(&S->net_inject_delay, lds_stat[SN_INJECT]);
+        // Network::transmit's per-packet router term (hops+1)*router, inject
+        // term and link remainder total - router - (plen-1) - inject, summed
+        // (mod 2^64, as the per-packet sums are)
+        const uint64_t acc = lds_stat[SN_ACC], dist = lds_stat[SN_DIST], tot = lds_stat[SN_TOTAL];
+        const uint64_t rt = (dist + acc) * (uint64_t)(uint32_t)g->router_delay;
+        const uint64_t inj = acc * (uint64_t)(uint32_t)g->inject_delay;
+        atomic_add_u64(&S->net_accesses, acc);
+        atomic_add_u64(&S->net_distance, dist);
+        atomic_add_u64(&S->net_total_delay, tot);
+        atomic_add_u64(&S->net_router_delay, rt);
+        atomic_add_u64(&S->net_link_delay, tot - rt - (lds_stat[SN_PLEN] - acc) - inj);
+        atomic_add_u64(&S->net_inject_delay, inj);
         atomic_add_u64(&S->dram_accesses, lds_stat[SN_DRAM]);
         atomic_add_u64(&S->total_bus_contention, lds_stat[SN_BUSCONT]);
         atomic_add_u64(reinterpret_cast<uint64_t*>(&S->total_num_broadcast), lds_stat[SN_BCAST]);
