@@ -207,7 +207,7 @@ __device__ __forceinline__ void err_or(uint64_t f) {
 enum ProfId {
     PF_LOOP, PF_REQ, PF_NET, PF_NSETUP, PF_NHOPS, PF_NTREE, PF_NWAIT, PF_NWB, PF_SETL0, PF_SETLN, PF_HOME_LD,
     PF_HOME, PF_DOWN, PF_WINDOWS, PF_TREEHOPS, PF_DEMAND, PF_T_LDS, PF_T_SEARCH, PF_T_DECIDE, PF_T_EDIT,
-    PF_T_STORE, PF_T_REFILL, PF_COUNT
+    PF_T_STORE, PF_T_REFILL, PF_NPRE, PF_NPOST, PF_COUNT
 };
 #ifdef PU_PROF
 static __shared__ unsigned long long lds_prof[PF_COUNT];
@@ -763,6 +763,7 @@ static __shared__ uint32_t lds_dir_w[2][32];
 template <bool LH>
 __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char* base_in, int src, int dst, int len,
                                                  uint64_t timer) {
+    PROF_T(p_pre);
     NetCtx c;
     AS1 char* base = (AS1 char*)(char*)uni64((uint64_t)base_in);
     c.qhdr = base + g->off_qhdr;
@@ -796,6 +797,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
     const int hops = hx + hy + hz;
     uint64_t t = timer + c.inject;
     uint64_t mg1 = 0, err = 0;
+    PROF_ADD(PF_NPRE, p_pre);
     for (int b0 = 0; b0 < hops; b0 += 64) {
         PROF_T(p_setup);
         PROF_CNT(PF_WINDOWS, 1);
@@ -928,6 +930,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         // see the stores).
         PROF_ADD(PF_NWB, p_wb);
     }
+    PROF_T(p_post);
     t += c.router;
     t += (uint64_t)(plen - 1);
     const uint64_t dist = (uint64_t)hops;
@@ -947,6 +950,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         lds_add_u64_lanes(lds_u32addr(&lds_stat[0]) + 8u * (uint32_t)ln, ((uint64_t)hi << 32) | lo, SN_NET_LANES);
     }
     if (err) err_or(err);
+    PROF_ADD(PF_NPOST, p_post);
     return t - timer;
 }
 

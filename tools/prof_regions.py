@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF_LIB = os.path.join(ROOT, "primesim_amd", "libprimeuncore_prof.so")
 NAMES = ["LOOP", "REQ", "NET", "NSETUP", "NHOPS", "NTREE", "NWAIT", "NWB", "SETL0", "SETLN", "HOME_LD",
          "HOME", "DOWN", "windows", "tree_hops", "demand_hops", "T_LDS", "T_SEARCH", "T_DECIDE", "T_EDIT",
-         "T_STORE", "T_REFILL"]
+         "T_STORE", "T_REFILL", "NPRE", "NPOST"]
 COUNTS = {"windows", "tree_hops", "demand_hops"}
 
 
