@@ -574,7 +574,7 @@ def main() -> None:
                 "kernel": "uncore_kernel<1, true, false>",
                 "avg_launch_ms": avg_ms,
                 "alg_bytes_per_launch": bytes_per_launch,
-                "limiter": "instruction issue and dependent-load latency (profiles/r2s3_sq_counters.json: 24% of wave cycles issuing, 52% waiting on memory, 25% in issue stalls at 5 waves/SIMD), not HBM bandwidth",
+                "limiter": "instruction issue and dependent-load latency (profiles/r2s3_h64_sq_counters.json: 25% of wave cycles issuing, 51% waiting on memory, 23% in issue stalls at 5 waves/SIMD), not HBM bandwidth",
             },
             "cpu_baseline": cpu,
             "cpu_baseline_ensemble": ens_res,

@@ -1931,9 +1931,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
     e.ln = lane_id();
     e.base = arena + (size_t)(replica0 + (int)blockIdx.x) * g->replica_bytes;
     if constexpr (LH) {                                   // the replica's queue headers into LDS
+        // LDS keeps the three 16-B pieces of each header (48-B slots)
         const AS1 v4u32* gh = (const AS1 v4u32*)(AS1 char*)(e.base + g->off_qhdr);
-        const uint32_t nq4 = (uint32_t)g->nqueues * (uint32_t)(sizeof(QueueHdr) / 16);
-        for (uint32_t k = (uint32_t)e.ln; k < nq4; k += 64) lds_qhdr[k] = gh[k];
+        const uint32_t nq3 = (uint32_t)g->nqueues * 3u;
+        for (uint32_t k = (uint32_t)e.ln; k < nq3; k += 64) lds_qhdr[k] = gh[(k / 3u) * PU_HDR_PIECES + k % 3u];
     }
     stats_init();
     e.dly = 0;
@@ -2020,8 +2021,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
     if constexpr (LH) {                                   // ... and back
         __syncthreads();
         AS1 v4u32* gh = (AS1 v4u32*)(AS1 char*)(e.base + g->off_qhdr);
-        const uint32_t nq4 = (uint32_t)g->nqueues * (uint32_t)(sizeof(QueueHdr) / 16);
-        for (uint32_t k = (uint32_t)e.ln; k < nq4; k += 64) gh[k] = lds_qhdr[k];
+        const uint32_t nq3 = (uint32_t)g->nqueues * 3u;
+        for (uint32_t k = (uint32_t)e.ln; k < nq3; k += 64) gh[(k / 3u) * PU_HDR_PIECES + k % 3u] = lds_qhdr[k];
     }
     if (e.ln == 0) {
         if (pos) pos[blockIdx.x] = i;
@@ -2189,7 +2190,7 @@ extern "C" int pu_engine_occupancy(int num_levels, int* blocks_per_cu) {
 }
 
 // Queue headers of one replica that fit the latency-mode LDS image.
-extern "C" int pu_engine_lds_header_queues(void) { return PU_LDS_QHDR_BYTES / (int)sizeof(QueueHdr); }
+extern "C" int pu_engine_lds_header_queues(void) { return PU_LDS_QHDR_BYTES / 48; }   // 48-B LDS slots
 
 extern "C" int pu_engine_init_queues(char* arena, uint64_t replica_bytes, uint64_t off_qhdr, uint64_t off_qring,
                                      int nqueues, int nreplicas, hipStream_t stream) {

@@ -19,9 +19,9 @@
 //     pool     : pool_entries x nwords x u64 bitmaps + a free stack
 //     dalive, dcnt : per slice
 //   queues (Graphite history tree restated as a ring of sorted free intervals):
-//     qhdr : nqueues x QueueHdr (48 B: M/G/1 moments, ring cursor and the first
-//            interval start, so the M/G/1-vs-tree decision of a hop needs the
-//            header only)  — links first, then per-cache buses
+//     qhdr : nqueues x QueueHdr (48 B in a 64-B line: M/G/1 moments, ring cursor
+//            and the first interval start, so the M/G/1-vs-tree decision of a
+//            hop needs the header only)  — links first, then per-cache buses
 //     qring: nqueues x 128 x {first,second} (2 KB)
 //   dram : banks x DramBank (opt-in bank model, pu_dram_cfg; absent when off)
 //   stats (EngineStats), per-core completion cycles, run state.
@@ -89,6 +89,7 @@ struct QueueHdr {
     double sum_sq;     // _sigma_service_time_square
     uint64_t newest;   // _newest_arrival_time
     uint64_t f0;       // ring[head].first: the tree's minimum key (the M/G/1 test)
+    uint64_t pad[2];   // one header per 64-B line: a visit reads and writes one line, not two
 };
 
 struct QueueSlot {
@@ -196,4 +197,5 @@ struct RunState {
     int64_t msg_shift;     // PU_KF_CLOSED: the open message's core shift at its first request
     uint64_t dead_tags;    // PU_KF_MSGHALT: receive threads (pu_req.tag < 64) that have exited
 };
-static_assert(sizeof(QueueHdr) == 48, "QueueHdr is three 16-B pieces");
+static_assert(sizeof(QueueHdr) == 64, "QueueHdr is three 16-B pieces in a 64-B line");
+constexpr uint32_t PU_HDR_PIECES = (uint32_t)(sizeof(QueueHdr) / 16);   // 16-B pieces per header in HBM
