@@ -1355,9 +1355,14 @@ struct Engine {
         const bool mine = (uint64_t)ln < D.nways;
         DirLine m;
         if (staged == 1) {
-            // staged before a transmit that ran hops: it issued at least 8 vector-
-            // memory operations since (4 header loads, 4 header stores)
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            // staged before a transmit that ran hops.  With headers in HBM that
+            // transmit waited for its first header load, and vector memory
+            // returns in issue order, so the staging DMA has landed (the
+            // vmcnt(8) only bounds it).  With headers in LDS (latency mode) an
+            // M/G/1-only transmit issues no vector memory operation at all:
+            // wait for the DMA itself.
+            if constexpr (LH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         } else if (staged == 2) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
