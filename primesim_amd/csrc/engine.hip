@@ -1004,7 +1004,8 @@ struct Engine {
                                              uint64_t cache_index, uint64_t addr) const {
         v.set = set_index(addr, offbits, nsets);
         v.tag = addr >> (offbits + idxbits);
-        v.line0 = (cache_index * nsets + v.set) * nways;
+        // 32-bit index math: a level holds fewer than 2^32 lines (pu_create checks)
+        v.line0 = (uint64_t)(((uint32_t)cache_index * (uint32_t)nsets + (uint32_t)v.set) * (uint32_t)nways);
         if ((uint64_t)ln < nways) {
             LineMeta m = meta[v.line0 + (uint64_t)ln];
             v.mtag = m.tag;
@@ -1325,7 +1326,7 @@ struct Engine {
         const DirGeo& D = g->dir;
         if (D.nways > 32) return 0;
         const uint64_t set = set_index(addr, D.offbits, D.nsets);
-        const uint64_t line0 = ((uint64_t)home * D.csets + (set >> D.cset_shift)) * D.nways;
+        const uint64_t line0 = (uint64_t)(((uint32_t)home * (uint32_t)D.csets + (uint32_t)(set >> D.cset_shift)) * (uint32_t)D.nways);
         if ((uint64_t)ln < D.nways) {
             const AS1 char* lp = (const AS1 char*)(const char*)(at<DirLine>(D.off_line) + line0 + (uint64_t)ln);
             lds_dma<true>(lp, lds_addr(&lds_dir_a[0]));
@@ -1351,7 +1352,7 @@ struct Engine {
         if (ln == (home & 63)) at<uint32_t>(D.off_alive)[home] = 1u;   // home_stat[home] = 1
         const uint64_t set = set_index(r.addr, D.offbits, D.nsets);
         const uint64_t tag = r.addr >> (D.offbits + D.idxbits);
-        const uint64_t line0 = ((uint64_t)home * D.csets + (set >> D.cset_shift)) * D.nways;   // reachable sets only
+        const uint64_t line0 = (uint64_t)(((uint32_t)home * (uint32_t)D.csets + (uint32_t)(set >> D.cset_shift)) * (uint32_t)D.nways);
         const bool mine = (uint64_t)ln < D.nways;
         DirLine m;
         if (staged == 1) {

@@ -217,6 +217,7 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
     for (int l = 0; l < y.num_levels; l++) {
         LevelGeo& L = g->lv[l];
         uint64_t lines = (uint64_t)L.ncaches * L.nsets * L.nways;
+        if (lines >= (1ull << 32)) return pu::set_error(PU_ENOTSUP, "at most 2^32 lines per cache level");
         L.off_meta = lay.take(lines * sizeof(LineMeta));
         L.off_ts = lay.take(lines * sizeof(int64_t));
         L.off_alive = lay.take((uint64_t)L.ncaches * 4);
@@ -225,6 +226,7 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
     // the bus system has no directory lines (its report still prints the
     // directory block, from counters that stay 0)
     uint64_t dlines = bus_sys ? 0 : (uint64_t)N * D.csets * D.nways;
+    if (dlines >= (1ull << 32)) return pu::set_error(PU_ENOTSUP, "at most 2^32 directory lines");
     D.off_line = lay.take(dlines * sizeof(DirLine));
     D.off_prog = lay.take(dlines * sizeof(int32_t));
     // sharer sets of more than 4 LLCs live in pool bitmaps: one entry per
@@ -247,6 +249,7 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
     if (y.tlb_enable) {
         TlbGeo& T = g->tlb;
         const uint64_t tl = (uint64_t)y.num_cores * T.nsets * T.nways;
+        if (tl >= (1ull << 32)) return pu::set_error(PU_ENOTSUP, "at most 2^32 TLB entries");
         T.off_meta = lay.take(tl * sizeof(LineMeta));
         T.off_ts = lay.take(tl * sizeof(int64_t));
         T.off_ppage = lay.take(tl * sizeof(uint64_t));

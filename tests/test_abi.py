@@ -58,6 +58,8 @@ def test_no_gpu_fails_loudly():
     (lambda s: s["system"].update(protocol_type=1, num_levels=2,
                                   cache=s["system"]["cache"] + [dict(s["system"]["cache"][0], share=4, level=1)]),
      "limited-pointer"),
+    # the engine indexes a level's lines in 32 bits: 16 L1s of 2^36 B / 64 B = 2^34 lines
+    (lambda s: s["system"]["cache"][0].update(size=1 << 36), "2^32 lines"),
 ])
 def test_config_validation_before_device(mutate, msg):
     sim = CF.preset("C1")
