@@ -498,7 +498,7 @@ def main() -> None:
         if single:
             log(f"[bench] single instance: {single['value']:.0f} accesses/s")
         cpu = None
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:          # the CPU baseline runs at N=1 only
             # replica 0's stream: the reference fills the warmup untimed, then is
             # timed on the requests of the GPU's timed window (as many as fit in
             # --cpu-seconds); parity is checked on every request both ran
@@ -578,7 +578,7 @@ def main() -> None:
             },
             "cpu_baseline": cpu,
             "cpu_baseline_ensemble": ens_res,
-            "parity": parity_ok if not args.no_cpu else None,
+            "parity": parity_ok if (not args.no_cpu and world == 1) else None,
         }
         print(json.dumps(result), flush=True)
     else:
