@@ -58,12 +58,16 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
+LAUNCH_CMD = None       # rank command for launch_ranks (None: this file; tests point it at a stub)
 LAST_REPLICAS = 0       # replicas of the last main() run (tools/prof_regions.py)
 LAST_PER_REPLICA = None  # per-replica stat deltas of the timed steps (profiling runs only)
 METRIC = "simulated memory accesses/sec (uncore) at 1024 cores; % HBM roofline"
+LIMITER = ("instruction issue and dependent-load latency (profiles/r2s3_fin3_sq.json: 25% of wave cycles issuing, "
+           "52% waiting on memory, 23% in issue stalls at 5 waves/SIMD), not HBM bandwidth")
 REQ_BYTES = 32          # sizeof(pu_req)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 SEED_BASE = 4
+STAGE_GROUP = 256       # replicas whose requests the host generates per staging copy
 
 
 def log(*a):
@@ -256,15 +260,23 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
     sptr = stream.cuda_stream
     um.set_replay_mode(replay)
     specs = [stream_spec(replica_seed(SEED_BASE, rank, r)) for r in range(R)]
-    gen = P.StreamSet(specs)
-    host = np.zeros((R, args.chunk), dtype=A.REQ_DTYPE)
+    # the host generates STAGE_GROUP replicas' chunks at a time into one reused
+    # buffer (335 MB at the default chunk), so 8 ranks of 5,120 replicas each
+    # hold ~3 GB of host staging in all instead of 6.7 GB per rank
+    G = min(R, STAGE_GROUP)
+    gens = [P.StreamSet(specs[g:g + G]) for g in range(0, R, G)]
+    host = np.zeros((G, args.chunk), dtype=A.REQ_DTYPE)
     offs = torch.from_numpy((np.arange(R + 1, dtype=np.uint64) * np.uint64(args.chunk)).view(np.int64)).to(dev)
     rep0 = []
 
     def next_chunk() -> torch.Tensor:
-        got = gen.next_into(host)
-        assert got == args.chunk, (got, args.chunk)
-        return torch.from_numpy(host.view(np.uint8).reshape(-1)).to(dev)
+        out = torch.empty((R, args.chunk * REQ_BYTES), dtype=torch.uint8, device=dev)
+        for k, gen in enumerate(gens):
+            n = len(gen)
+            got = gen.next_into(host[:n])
+            assert got == args.chunk, (got, args.chunk)
+            out[k * G:k * G + n].copy_(torch.from_numpy(host[:n].view(np.uint8).reshape(n, -1)))
+        return out.view(-1)
 
     d_warm_delay = torch.zeros(R * args.chunk, dtype=torch.int32, device=dev)
     t_w = time.time()
@@ -283,7 +295,8 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
     d_win = torch.empty((R, W_t, REQ_BYTES), dtype=torch.uint8, device=dev)
     for k in range(steps):
         d_win[:, k * args.chunk:(k + 1) * args.chunk, :] = next_chunk().view(R, args.chunk, REQ_BYTES)
-    gen.close()
+    for gen in gens:
+        gen.close()
     d_win_delay = torch.zeros(R * W_t, dtype=torch.int32, device=dev)
     win_off = np.arange(R + 1, dtype=np.uint64) * np.uint64(W_t)
     d_win_off = torch.from_numpy(win_off.view(np.int64)).to(dev)
@@ -338,7 +351,7 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
                 steps=steps, processed=int(delta["requests"]))
 
 
-def single_instance(cfg, args, dev, threads) -> dict:
+def single_instance(cfg, args, dev, threads, replay: int = 0) -> dict:
     """ONE simulation alone on the GPU: replica 0's stream, the same warmup,
     then --single-requests requests in one launch (HIP events)."""
     import torch
@@ -349,6 +362,7 @@ def single_instance(cfg, args, dev, threads) -> dict:
     reqs = P.generate_stream(stream_spec(replica_seed(SEED_BASE, 0, 0), n_w + n_t))
     um = P.UncoreManager()
     um.init(cfg, replicas=1, device=dev.index)
+    um.set_replay_mode(replay)
     for prog, th in threads:
         um.allocCore(prog, th)
     stream = torch.cuda.Stream(dev)
@@ -359,6 +373,7 @@ def single_instance(cfg, args, dev, threads) -> dict:
     pos = torch.tensor([n_w], dtype=torch.int64, device=dev)
     um.run_device(d_req.data_ptr(), off_w.data_ptr(), d_delay.data_ptr(), stream.cuda_stream)
     torch.cuda.synchronize(dev)
+    before = um.stats(0).as_dict()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
@@ -369,16 +384,65 @@ def single_instance(cfg, args, dev, threads) -> dict:
     ms = e0.elapsed_time(e1)
     st = um.stats(0).as_dict()
     um.close()
-    return {"value": n_t / (ms / 1e3), "unit": "accesses/s", "requests": n_t, "kernel_ms": ms, "wall_s": wall,
-            "sample": f"one C4 simulation alone on the GPU (replica 0's stream): {n_w} warmup requests, then "
-                      f"{n_t} requests in one launch; link visits/access {st['net_distance'] / st['requests']:.1f}",
-            "note": "one uncore is a sequential fold (one wavefront); DESIGN.md §8 measures how little of it a "
+    done = st["requests"] - before["requests"]     # a halted replica stops counting
+    mode = "closed-loop" if replay else "open-loop"
+    return {"value": done / (ms / 1e3), "unit": "accesses/s", "requests": int(done), "kernel_ms": ms, "wall_s": wall,
+            "mg1_share_of_link_visits": (st["mg1_calls"] - before["mg1_calls"]) /
+                                        max(1, st["net_distance"] - before["net_distance"]),
+            "sample": f"one C4 simulation alone on the GPU (replica 0's stream, {mode}): {n_w} warmup requests, then "
+                      f"{n_t} requests in one launch; link visits/access "
+                      f"{(st['net_distance'] - before['net_distance']) / max(1, done):.1f}",
+            "note": "one uncore is a sequential fold (one wavefront); DESIGN.md §1a measures how little of it a "
                     "relaxation can parallelise"}
 
 
-def main() -> None:
+# ---------------------------------------------------------------- N > 1 launch
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv: list, child_cmd: list | None = None, timeout_s: float | None = None) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes (fresh
+    children, one per GPU, LOCAL_RANK = rank; no exec) with the env that
+    torch.distributed.run would give them, wait for all, and return the worst
+    exit code.  Called before this process touches the GPU.  Rank 0 prints
+    the JSON line on the inherited stdout."""
+    import subprocess
+    port = free_port()
+    cmd = child_cmd or LAUNCH_CMD or [sys.executable, os.path.abspath(__file__)]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([*cmd, *argv], env=env))
+    rc, t0 = 0, time.time()
+    try:
+        for p in procs:
+            left = None if timeout_s is None else max(1.0, timeout_s - (time.time() - t0))
+            c = p.wait(timeout=left)
+            if c != 0 and rc == 0:
+                rc = c
+                log(f"[bench] a rank exited with {c}; stopping the others")
+                for q in procs:
+                    if q.poll() is None:
+                        q.terminate()
+    finally:
+        for q in procs:                       # the exact children started here
+            if q.poll() is None:
+                q.kill()
+                q.wait()
+    return rc
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node; N > 1 without WORLD_SIZE starts N rank processes itself")
     ap.add_argument("--steps", type=int, default=10, help="timed steps")
     ap.add_argument("--warmup", type=int, default=10, help="untimed steps of --chunk requests per replica")
     ap.add_argument("--replicas", type=int, default=0, help="replicas per GPU (0 = size to HBM)")
@@ -396,11 +460,64 @@ def main() -> None:
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) normally; gloo for CPU-side rehearsal")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC traffic summary written by tools/pmc_traffic.py for this build")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+class Device:
+    """This rank's GPU, engine handle and stream (bench's only device state)."""
+
+    def __init__(self, args, cfg, threads, rank: int, local: int):
+        import torch
+
+        import primesim_amd as P
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+        # ---- per-replica HBM: engine state + the timed request slabs + one warmup chunk
+        probe = P.UncoreManager()
+        probe.init(cfg, replicas=1, device=local)
+        rbytes = probe.replica_bytes
+        resident = probe.resident_replicas
+        probe.close()
+        # ranks rehearsed on one card (PU_BENCH_DEVICE) split its memory and waves
+        share = int(os.environ.get("LOCAL_WORLD_SIZE", "1")) if "PU_BENCH_DEVICE" in os.environ else 1
+        per_bytes = rbytes + (args.steps + 1) * args.chunk * (REQ_BYTES + 4)
+        free, _ = torch.cuda.mem_get_info(self.dev)
+        # as many replicas as fit in HBM, but no more than the kernel keeps resident
+        # (one wave each): a time-sliced launch over more would run in two rounds
+        R = args.replicas or max(1, min(resident // share, int((free * 0.88 / share) // per_bytes)))
+        R = max(1, R - R % 8) if R >= 8 else R
+        log(f"[bench] rank {rank}: replica {rbytes / 2**20:.0f} MiB + requests {(per_bytes - rbytes) / 2**20:.0f} MiB, "
+            f"{R} replicas (resident limit {resident}), free {free / 2**30:.0f} GiB")
+        self.R = R
+        self.um = P.UncoreManager()
+        self.um.init(cfg, replicas=R, device=local)
+        for prog, th in threads:
+            self.um.allocCore(prog, th)
+        self.stream = torch.cuda.Stream(self.dev)
+        assert self.stream.cuda_stream != 0
+
+    def headline(self, args, rank: int, world: int):
+        import primesim_amd as P
+        return run_pass(self.um, args, self.R, rank, world, self.dev, self.stream, P.uncore.PU_REPLAY_OPEN, args.steps,
+                        keep_rep0=rank == 0)
+
+    def reduce_device(self, args):
+        """Where the max/sum reduction's tensors live: the GPU under RCCL."""
+        return self.dev if args.dist_backend == "nccl" else None
+
+
+def main(argv=None) -> None:
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # before any GPU call: this process only waits for its N ranks
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:] if argv is None else list(argv)))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        log(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a {world}-rank run "
+            f"as {args.gpus} GPUs")
+        sys.exit(2)
     extras = rank == 0 and world == 1 and not args.no_extras
 
     import primesim_amd as P
@@ -420,42 +537,21 @@ def main() -> None:
         nw = args.ensemble_workers or host_core_share()
         ens = Ensemble(xml_path, nw, args.warmup * args.chunk, args.steps * args.chunk, args.ensemble_seconds)
 
-    import torch
     import torch.distributed as dist
     if world > 1:
         dist.init_process_group(args.dist_backend, init_method="env://")
     # PU_BENCH_DEVICE pins every rank to one card (rehearsing N>1 on a 1-GPU box)
     local = int(os.environ.get("PU_BENCH_DEVICE", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
-    # ---- per-replica HBM: engine state + the timed request slabs + one warmup chunk
-    probe = P.UncoreManager()
-    probe.init(cfg, replicas=1, device=local)
-    rbytes = probe.replica_bytes
-    resident = probe.resident_replicas
-    probe.close()
-    per_bytes = rbytes + (args.steps + 1) * args.chunk * (REQ_BYTES + 4)
-    free, total = torch.cuda.mem_get_info(dev)
-    # as many replicas as fit in HBM, but no more than the kernel keeps resident
-    # (one wave each): a time-sliced launch over more would run in two rounds
-    R = args.replicas or max(1, min(resident, int((free * 0.88) // per_bytes)))
-    R = max(1, R - R % 8) if R >= 8 else R
-    log(f"[bench] rank {rank}: replica {rbytes / 2**20:.0f} MiB + requests {(per_bytes - rbytes) / 2**20:.0f} MiB, "
-        f"{R} replicas (resident limit {resident}), free {free / 2**30:.0f} GiB")
+    D = Device(args, cfg, threads, rank, local)
+    R, um, dev, stream = D.R, D.um, D.dev, D.stream
     global LAST_REPLICAS, LAST_PER_REPLICA
     LAST_REPLICAS = R
-    um = P.UncoreManager()
-    um.init(cfg, replicas=R, device=local)
-    for prog, th in threads:
-        um.allocCore(prog, th)
-    stream = torch.cuda.Stream(dev)
-    assert stream.cuda_stream != 0
 
     # ---- headline: open-loop replay
-    H = run_pass(um, args, R, rank, world, dev, stream, P.uncore.PU_REPLAY_OPEN, args.steps, keep_rep0=rank == 0)
+    H = D.headline(args, rank, world)
     LAST_PER_REPLICA = H.per_replica
-    t_max, tot_processed = reduce_run(H.elapsed, H.processed, dev if args.dist_backend == "nccl" else None)
+    t_max, tot_processed = reduce_run(H.elapsed, H.processed, D.reduce_device(args))
+    _, tot_replicas = reduce_run(0.0, R, D.reduce_device(args))
     value = tot_processed / t_max
     avg_ms = float(np.mean(H.kern_ms))
     bytes_per_launch = alg_bytes(H.delta, cfg) / args.steps
@@ -473,7 +569,7 @@ def main() -> None:
             um.reset()
             C = run_pass(um, args, R, rank, world, dev, stream, P.uncore.PU_REPLAY_CLOSED, args.closed_steps,
                          keep_rep0=True)
-            c_par = None
+            c_par, c_cpu = None, None
             if not args.no_cpu:
                 import oracle as O
                 w0, n_t = args.warmup * args.chunk, args.closed_steps * args.chunk
@@ -483,12 +579,20 @@ def main() -> None:
                 m = min(len(d_cpu), len(gd))
                 c_par = {"kind": kind, "requests_compared": m, "bit_identical": bool(np.array_equal(gd[:m], d_cpu[:m]))}
                 parity_ok &= c_par["bit_identical"]
+                c_cpu = {"value": n_cpu / el, "unit": "accesses/s", "cores": 1, "kind": kind, "cpu_model": cpu_model(),
+                         "sample": f"replica 0's C4 stream replayed closed-loop: requests {w0}..{w0 + n_cpu} after an "
+                                   f"untimed closed-loop fill of {w0}, single-threaded "
+                                   f"({'reference uncore compiled from /root/reference/src' if kind == 'reference' else 'oracle/cpu_ref restatement'}), "
+                                   f"{el:.1f} s"}
+                log(f"[bench] closed-loop cpu baseline ({kind}): {n_cpu / el:.0f} accesses/s")
             closed = {"value": C.processed / C.elapsed, "unit": "accesses/s", "steps": C.steps,
                       "per_simulation_accesses_per_s": C.processed / C.elapsed / R,
                       "halted_replicas": C.halted,
                       "mg1_share_of_link_visits": C.delta["mg1_calls"] / max(1, C.delta["net_distance"]),
                       "mean_delay_cycles": 0.0,
-                      "parity": c_par}
+                      "parity": c_par,
+                      "cpu_baseline": c_cpu,
+                      "single_instance": None}
             gd = np.concatenate(C.rep0)
             closed["mean_delay_cycles"] = float(gd[gd != 0].mean()) if (gd != 0).any() else 0.0
             log(f"[bench] closed loop: {closed['value']:.4g} accesses/s, halted {C.halted}, "
@@ -497,6 +601,9 @@ def main() -> None:
         single = single_instance(cfg, args, dev, threads) if extras else None
         if single:
             log(f"[bench] single instance: {single['value']:.0f} accesses/s")
+        if closed is not None:
+            closed["single_instance"] = single_instance(cfg, args, dev, threads, P.uncore.PU_REPLAY_CLOSED)
+            log(f"[bench] closed-loop single instance: {closed['single_instance']['value']:.0f} accesses/s")
         cpu = None
         if not args.no_cpu and world == 1:          # the CPU baseline runs at N=1 only
             # replica 0's stream: the reference fills the warmup untimed, then is
@@ -549,18 +656,22 @@ def main() -> None:
                 "workload": "C4: 1024-core 32x32 mesh, L1 32KB/8W + 256KB/8W shared-LLC slice per tile, "
                             "directory MESI full-map, uniform 2^20 lines + 64-line hotspot, 25% writes, open-loop replay",
                 "replicas_per_gpu": R,
+                "replicas_total": tot_replicas,
                 "step": (f"wall-time slice: every replica continues its own stream for {args.slice_ms:g} ms per "
                          f"launch, stopping only between requests" if args.slice_ms > 0 else
                          f"fixed: {args.chunk} requests per replica per launch"),
                 "mean_requests_per_replica_per_step": H.processed / (R * args.steps),
                 "warmup_requests_per_replica": args.warmup * args.chunk,
-                "parallelism": f"replicas: {R} independent uncores per GPU x {world} GPU(s)",
+                "parallelism": (f"replicas: {R} independent uncores per GPU x {world} GPU(s), one process per GPU, "
+                                f"no data-path collective ({args.dist_backend} for the barrier and the max/sum "
+                                f"reduction only)" if world > 1 else
+                                f"replicas: {R} independent uncores on 1 GPU"),
                 "halted_replicas": H.halted,
                 "mg1_share_of_link_visits": H.delta["mg1_calls"] / max(1, H.delta["net_distance"]),
                 "error_flags": H.errf & ~A.PU_ERRF_NEG_DELAY,
                 "engine_build": P.uncore.library_source_hash(),
             },
-            "per_simulation_accesses_per_s": value / (R * world),
+            "per_simulation_accesses_per_s": value / tot_replicas,
             "single_instance": single,
             "closed_loop": closed,
             "roofline": {
@@ -574,7 +685,7 @@ def main() -> None:
                 "kernel": "uncore_kernel<1, true, false>",
                 "avg_launch_ms": avg_ms,
                 "alg_bytes_per_launch": bytes_per_launch,
-                "limiter": "instruction issue and dependent-load latency (profiles/r2s3_h64_sq_counters.json: 25% of wave cycles issuing, 51% waiting on memory, 23% in issue stalls at 5 waves/SIMD), not HBM bandwidth",
+                "limiter": LIMITER,
             },
             "cpu_baseline": cpu,
             "cpu_baseline_ensemble": ens_res,

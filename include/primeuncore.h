@@ -274,6 +274,13 @@ int pu_error_flags(pu_handle* h, uint64_t* out, size_t n);
  * closed-loop shift apply here: those belong to the caller's message loop. */
 int pu_access(pu_handle* h, int core_id, int prog_id, int mem_type,
               uint64_t* addr, int64_t timer);
+/* The same with the status out of band: returns 0 or PU_E*, and the delay
+ * (any int, including a wrapped negative one, or -1 for core_id >= num_cores)
+ * goes to *delay_out.  pu_access reports errors in-band, so a wrapped delay
+ * that happens to equal a PU_E* code is ambiguous there; the C++ and Python
+ * mirrors use this entry point. */
+int pu_access_status(pu_handle* h, int core_id, int prog_id, int mem_type,
+                     uint64_t* addr, int64_t timer, int32_t* delay_out);
 
 /* Batch path from host memory: the per-message loop of prime.cpp:120-137 for
  * replica `replica`.  delay_out[i] receives uncore_access's return value for

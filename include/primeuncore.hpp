@@ -12,6 +12,7 @@
 #include <ostream>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "primeuncore.h"
@@ -44,6 +45,64 @@ class UncoreManager {
     UncoreManager& operator=(const UncoreManager&) = delete;
     ~UncoreManager() { pu_destroy(h_); }
 
+    // The reference's config structs (XmlSim / XmlSys / XmlCache / XmlNetwork,
+    // reference src/xml_parser.h:43-100) copied field by field into the C ABI's
+    // pu_sim_cfg.  A template over the struct, so this header includes no
+    // reference header: any type with those member names converts (prime.cpp's
+    // XmlSim from XmlParser::getXmlSim, xml_parser.cpp:121).  XmlSys::cache
+    // points to num_levels XmlCache entries (xml_parser.cpp:605-681).
+    template <class XmlSimT>
+    static pu_sim_cfg config_from(const XmlSimT& xs) {
+        if (xs.sys.num_levels < 1 || xs.sys.num_levels > PU_MAX_LEVELS)
+            throw std::runtime_error("XmlSim: num_levels " + std::to_string(xs.sys.num_levels) +
+                                     " outside 1.." + std::to_string(PU_MAX_LEVELS));
+        pu_sim_cfg c;
+        std::memset(&c, 0, sizeof c);
+        c.max_msg_size = xs.max_msg_size;
+        c.num_recv_threads = xs.num_recv_threads;
+        c.thread_sync_interval = xs.thread_sync_interval;
+        c.proc_sync_interval = xs.proc_sync_interval;
+        c.syscall_cost = xs.syscall_cost;
+        const auto& y = xs.sys;
+        pu_sys_cfg& s = c.sys;
+        s.sys_type = y.sys_type;
+        s.protocol_type = y.protocol_type;
+        s.max_num_sharers = y.max_num_sharers;
+        s.page_size = y.page_size;
+        s.tlb_enable = y.tlb_enable;
+        s.shared_llc = y.shared_llc;
+        s.verbose_report = y.verbose_report;
+        s.dram_access_time = y.dram_access_time;
+        s.cpi_nonmem = y.cpi_nonmem;
+        s.num_levels = y.num_levels;
+        s.num_cores = y.num_cores;
+        s.freq = y.freq;
+        s.bus_latency = y.bus_latency;
+        s.page_miss_delay = y.page_miss_delay;
+        s.network.data_width = y.network.data_width;
+        s.network.header_flits = y.network.header_flits;
+        s.network.net_type = y.network.net_type;
+        s.network.router_delay = y.network.router_delay;
+        s.network.link_delay = y.network.link_delay;
+        s.network.inject_delay = y.network.inject_delay;
+        copy_cache(s.directory_cache, y.directory_cache);
+        copy_cache(s.tlb_cache, y.tlb_cache);
+        for (int l = 0; l < y.num_levels; l++) copy_cache(s.cache[l], y.cache[l]);
+        return c;   // s.dram stays 0: the reference's fixed-latency Dram
+    }
+
+    // UncoreManager::init(XmlSim*) (uncore_manager.h:54, uncore_manager.cpp:46-50):
+    // prime.cpp's `uncore_manager.init(xml_sim);` (prime.cpp:198) compiles
+    // unchanged.  Not selected for pu_sim_cfg (the overload below).
+    template <class XmlSimT,
+              typename std::enable_if<!std::is_same<typename std::remove_cv<XmlSimT>::type, pu_sim_cfg>::value,
+                                      int>::type = 0>
+    void init(XmlSimT* xml_sim, int replicas = 1, int device = 0) {
+        if (!xml_sim) throw std::runtime_error("UncoreManager::init: null XmlSim");
+        const pu_sim_cfg c = config_from(*xml_sim);
+        init(&c, replicas, device);
+    }
+
     // UncoreManager::init (uncore_manager.cpp:46-50); `replicas` independent uncores.
     void init(const pu_sim_cfg* cfg, int replicas = 1, int device = 0) {
         h_ = pu_create(cfg, replicas, device);
@@ -67,12 +126,16 @@ class UncoreManager {
 
     // UncoreManager::uncore_access (uncore_manager.cpp:82-85): -1 if core_id >=
     // num_cores; a negative value when the reference's int wraps; throws on an
-    // engine error (PU_E* codes).
-    int uncore_access(int core_id, InsMem* ins, int64_t timer) {
-        int d = pu_access(h_, core_id, ins->prog_id, ins->mem_type, &ins->addr_dmem, timer);
-        if (d == PU_EINVAL || d == PU_ENOMEM || d == PU_ENODEV || d == PU_ERANGE || d == PU_EIO ||
-            d == PU_ENOTSUP || d == PU_ESTATE)
-            throw std::runtime_error(pu_last_error());
+    // engine error (pu_access_status's out-of-band status).
+    // A template over the request struct: the reference's own InsMem (cache.h:92-99)
+    // works unchanged at prime.cpp:129, and so does pu::InsMem.
+    template <class InsMemT>
+    int uncore_access(int core_id, InsMemT* ins, int64_t timer) {
+        uint64_t a = ins->addr_dmem;
+        int32_t d = 0;
+        if (pu_access_status(h_, core_id, ins->prog_id, ins->mem_type, &a, timer, &d) != 0)
+            throw std::runtime_error(pu_last_error());   // status out of band: every int delay is a delay
+        ins->addr_dmem = a;
         return d;
     }
 
@@ -135,6 +198,16 @@ class UncoreManager {
     pu_handle* handle() { return h_; }
 
    private:
+    template <class XmlCacheT>
+    static void copy_cache(pu_cache_cfg& d, const XmlCacheT& x) {
+        d.level = x.level;
+        d.share = x.share;
+        d.access_time = x.access_time;
+        d.size = x.size;
+        d.block_size = x.block_size;
+        d.num_ways = x.num_ways;
+    }
+
     pu_handle* h_ = nullptr;
     int num_cores_ = 0;
     std::vector<pu_req> reqs_;

@@ -683,8 +683,18 @@ int pu_access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n, int
 }
 
 int pu_access(pu_handle* h, int core_id, int prog_id, int mem_type, uint64_t* addr, int64_t timer) {
-    if (!h || !addr) return pu::set_error(PU_EINVAL, "bad arguments");
-    if (core_id >= h->cfg.sys.num_cores) return -1;   // System::access, system.cpp:147-150
+    int32_t d = 0;
+    int rc = pu_access_status(h, core_id, prog_id, mem_type, addr, timer, &d);
+    return rc ? rc : d;
+}
+
+int pu_access_status(pu_handle* h, int core_id, int prog_id, int mem_type, uint64_t* addr, int64_t timer,
+                     int32_t* delay_out) {
+    if (!h || !addr || !delay_out) return pu::set_error(PU_EINVAL, "bad arguments");
+    if (core_id >= h->cfg.sys.num_cores) {              // System::access, system.cpp:147-150
+        *delay_out = -1;
+        return 0;
+    }
     pu_req r;
     std::memset(&r, 0, sizeof(r));
     r.addr = *addr;
@@ -699,7 +709,8 @@ int pu_access(pu_handle* h, int core_id, int prog_id, int mem_type, uint64_t* ad
     // with the TLB on, InsMem::addr_dmem comes back as the physical address (system.cpp:916)
     int rc = access_batch(h, 0, &r, 1, &d, PU_KF_NOHALT, h->geo.tlb_enable ? addr : nullptr);
     if (rc) return rc;
-    return d;
+    *delay_out = d;
+    return 0;
 }
 
 int pu_run_device(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay, void* hip_stream) {

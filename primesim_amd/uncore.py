@@ -64,6 +64,8 @@ def lib() -> C.CDLL:
         "pu_dealloc_core": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
         "pu_get_core_id": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
         "pu_access": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, P(C.c_uint64), C.c_int64]),
+        "pu_access_status": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, P(C.c_uint64), C.c_int64,
+                                       P(C.c_int32)]),
         "pu_access_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.c_void_p]),
         "pu_run_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
         "pu_run_device_sliced": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
@@ -128,8 +130,8 @@ def last_error() -> str:
     return lib().pu_last_error().decode()
 
 
-# PU_E* codes (include/primeuncore.h); any other negative pu_access value is a
-# delay that wrapped in the reference's `int`
+# PU_E* codes (include/primeuncore.h).  pu_access returns them in-band (a
+# wrapped delay may collide with one); the mirror uses pu_access_status.
 PU_ERRORS = (-5, -12, -19, -22, -34, -71, -95)
 PU_REPLAY_OPEN, PU_REPLAY_CLOSED = 0, 1
 
@@ -393,11 +395,13 @@ class UncoreManager:
     # UncoreManager::uncore_access (uncore_manager.cpp:82-85)
     def uncore_access(self, core_id: int, ins_mem: InsMem, timer: int) -> int:
         addr = C.c_uint64(ins_mem.addr_dmem)
-        d = lib().pu_access(self._handle(), core_id, ins_mem.prog_id, ins_mem.mem_type, C.byref(addr), timer)
-        if d in PU_ERRORS:
+        d = C.c_int32(0)
+        rc = lib().pu_access_status(self._handle(), core_id, ins_mem.prog_id, ins_mem.mem_type, C.byref(addr), timer,
+                                    C.byref(d))
+        if rc != 0:                       # status out of band: every int delay is a delay
             raise UncoreError(f"uncore_access: {last_error()}")
         ins_mem.addr_dmem = addr.value
-        return d
+        return d.value
 
     def access_batch(self, reqs: np.ndarray, replica: int = 0) -> np.ndarray:
         """prime.cpp:120-137 for a run of messages; returns per-request delays."""

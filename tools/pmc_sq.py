@@ -28,6 +28,8 @@ PASSES = [
     ["TCC_HIT_sum", "TCC_MISS_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_WRREQ_sum"],
     ["SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_INSTS_LDS"],
     ["SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU"],
+    ["SQ_INSTS_SMEM", "SQ_INSTS_BRANCH", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_MISC", "SQ_INSTS_SENDMSG"],
+    ["SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_TRANS_F64"],
 ]
 
 
@@ -35,6 +37,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", required=True)
     ap.add_argument("--work", default=os.path.join(ROOT, "gpurun_out", "pmc_sq"))
+    ap.add_argument("--kernel", default=KERNEL, help="kernel name substring to sum over")
     ap.add_argument("bench_args", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     bargs = [x for x in a.bench_args if x != "--"]
@@ -58,7 +61,7 @@ def main() -> None:
         for fn in files:
             with open(fn) as fh:
                 for row in csv.DictReader(fh):
-                    if KERNEL not in row.get("Kernel_Name", ""):
+                    if a.kernel not in row.get("Kernel_Name", ""):
                         continue
                     did = int(row["Dispatch_Id"])
                     vals.setdefault(row["Counter_Name"], {}).setdefault(did, 0.0)
