@@ -228,6 +228,11 @@ typedef struct pu_handle pu_handle;
  * Returns NULL on failure (see pu_last_error). */
 pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device);
 void       pu_destroy(pu_handle* h);
+/* The replica geometry the engine derives from cfg (layout offsets, set and
+ * mesh parameters) as C++ source: a constexpr `Geo kJitGeo = {...};` the engine
+ * can be specialised against (compile-time configuration).  Returns the full
+ * length like snprintf; no reference counterpart. */
+long pu_config_geo_source(const pu_sim_cfg* cfg, char* buf, size_t cap);
 /* Return all replicas to the just-initialised state (no reallocation). */
 int        pu_reset(pu_handle* h);
 int        pu_num_replicas(const pu_handle* h);
@@ -510,6 +515,13 @@ void pu_client_close(pu_client* c);
  * (queue_model_history_tree.cpp:42-125 + queue_model_m_g_1.cpp). */
 int pu_unit_queue_run(uint64_t min_proc, const uint64_t* t, const uint64_t* p, size_t n,
                       uint64_t* delay_out, uint64_t* mg1_calls, int device);
+/* QueueModelMG1::computeQueueDelay (queue_model_m_g_1.cpp:16-42) evaluated by
+ * the engine's M/G/1 arithmetic on n given queue states: state i is
+ * _num_arrivals = num_arrivals[i] (< 2^53), _sigma_service_time = sum[i],
+ * _sigma_service_time_square = sum_sq[i], _newest_arrival_time = newest[i];
+ * wait_out[i] = the queue delay.  The arithmetic fuzz of the M/G/1 branch. */
+int pu_unit_mg1_run(const uint64_t* num_arrivals, const double* sum, const double* sum_sq,
+                    const uint64_t* newest, size_t n, uint64_t* wait_out, int device);
 /* Network::transmit sequence on a fresh mesh (network.cpp:97-160); st gets
  * the network counters. */
 int pu_unit_network_run(int num_nodes, int net_type, int data_width, int header_flits,

@@ -45,6 +45,7 @@ def oracle_lib() -> C.CDLL:
         L.cpuref_set_mode.argtypes = [C.c_void_p, C.c_int]
         L.cpuref_completion.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.cpuref_cache_counters.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]
+        L.cpuref_mg1_batch.argtypes = [C.c_void_p] * 4 + [C.c_size_t, C.c_void_p]
         L.cpuref_queue_run.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
                                        P(C.c_uint64)]
         L.cpuref_network_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64,
@@ -79,6 +80,7 @@ def ref_lib() -> C.CDLL:
         L.ref_counters.argtypes = [C.c_void_p]
         L.ref_destroy.argtypes = [C.c_void_p]
         L.ref_queue_run.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.ref_mg1_batch.argtypes = [C.c_void_p] * 4 + [C.c_size_t, C.c_void_p]
         L.ref_network_run.restype = C.c_long
         L.ref_network_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64,
                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
@@ -218,6 +220,32 @@ class RefUncore:
         out = (C.c_uint64 * 7)()
         ref_lib().ref_counters(out)
         return dict(zip(REF_COUNTER_NAMES, [int(x) for x in out]))
+
+
+def _mg1_args(n, s, q, w):
+    n = np.ascontiguousarray(n, dtype=np.uint64)
+    s = np.ascontiguousarray(s, dtype=np.float64)
+    q = np.ascontiguousarray(q, dtype=np.float64)
+    w = np.ascontiguousarray(w, dtype=np.uint64)
+    assert len(n) == len(s) == len(q) == len(w)
+    return n, s, q, w
+
+
+def ref_mg1(n, s, q, w) -> np.ndarray:
+    """The reference's QueueModelMG1::computeQueueDelay on the states (n, Σs, Σs², newest)."""
+    n, s, q, w = _mg1_args(n, s, q, w)
+    out = np.zeros(len(n), dtype=np.uint64)
+    ref_lib().ref_mg1_batch(n.ctypes.data, s.ctypes.data, q.ctypes.data, w.ctypes.data, len(n), out.ctypes.data)
+    return out
+
+
+def cpuref_mg1(n, s, q, w) -> np.ndarray:
+    """The restatement's mg1_wait on the same states."""
+    n, s, q, w = _mg1_args(n, s, q, w)
+    out = np.zeros(len(n), dtype=np.uint64)
+    oracle_lib().cpuref_mg1_batch(n.ctypes.data, s.ctypes.data, q.ctypes.data, w.ctypes.data, len(n),
+                                  out.ctypes.data)
+    return out
 
 
 def ref_queue(min_proc: int, t: np.ndarray, p: np.ndarray) -> np.ndarray:

@@ -983,6 +983,20 @@ int cpuref_network_run(int num_nodes, int net_type, int data_width, int header_f
     return 0;
 }
 
+// mg1_wait on given states (tests/test_gpu_mg1.py, test_units_oracle.py)
+int cpuref_mg1_batch(const uint64_t* n, const double* sum, const double* sum_sq, const uint64_t* newest, size_t cnt,
+                     uint64_t* out) {
+    Queue q;
+    for (size_t i = 0; i < cnt; i++) {
+        q.n = n[i];
+        q.sum = sum[i];
+        q.sum_sq = sum_sq[i];
+        q.newest = newest[i];
+        out[i] = mg1_wait(q);
+    }
+    return 0;
+}
+
 int cpuref_queue_run(uint64_t min_proc, const uint64_t* t, const uint64_t* p, size_t n,
                      uint64_t* delay_out, uint64_t* mg1_calls) {
     Queue q;

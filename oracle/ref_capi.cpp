@@ -25,6 +25,7 @@
 #include "xml_parser.h"    // reference src/xml_parser.h
 #include "network.h"       // reference src/network.h
 #include "queue_model.h"   // reference src/Graphite/queue_model.h
+#include "queue_model_m_g_1.h"   // reference src/Graphite/queue_model_m_g_1.h
 
 #include "../include/primeuncore.h"
 
@@ -255,6 +256,31 @@ int ref_queue_run(uint64_t min_proc, const uint64_t* t, const uint64_t* p, size_
     for (size_t i = 0; i < n; i++) delay_out[i] = q->computeQueueDelay(t[i], p[i]);
     (void)before;
     delete q;
+    return 0;
+}
+
+// ---- unit: the reference's QueueModelMG1::computeQueueDelay (queue_model_m_g_1.cpp:16-42)
+// on given states.  Its four state members are private (queue_model_m_g_1.h:16-19);
+// a layout twin of that standard-layout class sets them on a constructed object.
+struct MG1Twin {
+    volatile double sigma_sq;   // _sigma_service_time_square
+    volatile double sigma;      // _sigma_service_time
+    UInt64 n;                   // _num_arrivals
+    UInt64 newest;              // _newest_arrival_time
+};
+static_assert(sizeof(MG1Twin) == sizeof(QueueModelMG1), "QueueModelMG1 layout (queue_model_m_g_1.h:16-19)");
+
+int ref_mg1_batch(const uint64_t* n, const double* sum, const double* sum_sq, const uint64_t* newest, size_t cnt,
+                  uint64_t* out) {
+    QueueModelMG1 q;
+    MG1Twin* t = reinterpret_cast<MG1Twin*>(&q);
+    for (size_t i = 0; i < cnt; i++) {
+        t->sigma_sq = sum_sq[i];
+        t->sigma = sum[i];
+        t->n = n[i];
+        t->newest = newest[i];
+        out[i] = q.computeQueueDelay(0, 1);
+    }
     return 0;
 }
 

@@ -14,9 +14,10 @@ namespace pu {
 int set_error(int code, const std::string& msg);
 
 // pu_run_device with extra kernel flags (PU_KF_*, geometry.h): the server's
-// per-receive-thread stop.
+// per-receive-thread stop.  use_replay_mode = false launches open-loop whatever
+// pu_set_replay_mode left on the handle (live clients' timers are real).
 int run_device_flags(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
-                     uint32_t extra_flags);
+                     uint32_t extra_flags, bool use_replay_mode = true);
 
 // ThreadSched (reference src/thread_sched.cpp:55-91) with its quirks: the
 // first free core is taken, a busy core is marked with its prog id, a core is

@@ -34,6 +34,17 @@
 
 namespace {
 
+// Compile-time configuration: built with -DPU_JIT_GEO='"file"' (a file written
+// by pu_config_geo_source: `__device__ constexpr Geo kJitGeo = {...};`) the
+// engine kernel reads its geometry from that constant instead of the Geo
+// argument, so every configuration value folds into the code.
+#ifdef PU_JIT_GEO
+#include PU_JIT_GEO
+#define PU_GEO(g) (&kJitGeo)
+#else
+#define PU_GEO(g) (g)
+#endif
+
 constexpr uint32_t ST_I = 0, ST_S = 1, ST_E = 2, ST_M = 3, ST_V = 4, ST_B = 5;
 
 __device__ __forceinline__ int lane_id() { return (int)threadIdx.x; }
@@ -1933,13 +1944,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
     }
     const uint64_t wave_t0 = __builtin_amdgcn_s_memrealtime();
     Engine<NL, LH> e;
-    e.g = g;
+    e.g = PU_GEO(g);
     e.ln = lane_id();
-    e.base = arena + (size_t)(replica0 + (int)blockIdx.x) * g->replica_bytes;
+    e.base = arena + (size_t)(replica0 + (int)blockIdx.x) * e.g->replica_bytes;
     if constexpr (LH) {                                   // the replica's queue headers into LDS
         // LDS keeps the three 16-B pieces of each header (48-B slots)
-        const AS1 v4u32* gh = (const AS1 v4u32*)(AS1 char*)(e.base + g->off_qhdr);
-        const uint32_t nq3 = (uint32_t)g->nqueues * 3u;
+        const AS1 v4u32* gh = (const AS1 v4u32*)(AS1 char*)(e.base + e.g->off_qhdr);
+        const uint32_t nq3 = (uint32_t)e.g->nqueues * 3u;
         for (uint32_t k = (uint32_t)e.ln; k < nq3; k += 64) lds_qhdr[k] = gh[(k / 3u) * PU_HDR_PIECES + k % 3u];
     }
     stats_init();
@@ -1952,7 +1963,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
     // The message loop's own state lives in LDS (lane 0 writes, every lane reads
     // it back wave-uniform): nothing of it stays in registers across the
     // inlined access(), whose register budget is tight (4 waves/SIMD).
-    RunState* rs = e.template at<RunState>(g->off_run);
+    RunState* rs = e.template at<RunState>(e.g->off_run);
     if (e.ln == 0) {
         const int32_t h0 = rs->halted;
         lds_ctl.D = rs->batch_delay;
@@ -1978,13 +1989,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
         }
         PROF_T(p_loop);
         const pu_req q = reqs[i];
-        const bool core_ok = q.core >= 0 && q.core < g->num_cores;
+        const bool core_ok = q.core >= 0 && q.core < e.g->num_cores;
         const uint32_t fl = uni32(lds_ctl.flags);
         if (q.batch_start && e.ln == 0) {
             lds_ctl.D = 0;
             lds_ctl.skip = (fl & PU_KF_MSGHALT) ? (int32_t)((lds_ctl.dead_tags >> (q.tag & 63)) & 1) : 0;
             if ((fl & PU_KF_CLOSED) && core_ok)
-                lds_ctl.msg_shift = e.template at<int64_t>(g->off_core_shift)[q.core];
+                lds_ctl.msg_shift = e.template at<int64_t>(e.g->off_core_shift)[q.core];
         }
         __builtin_amdgcn_wave_barrier();
         if (uni32((uint32_t)lds_ctl.skip)) {     // PU_KF_MSGHALT: this message's receive thread has exited
@@ -2002,9 +2013,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
             lds_ctl.done++;
             delays[i] = d;
             if (core_ok) {
-                e.template at<int64_t>(g->off_completion)[q.core] = t + d;
+                e.template at<int64_t>(e.g->off_completion)[q.core] = t + d;
                 if (lds_ctl.flags & PU_KF_CLOSED)
-                    e.template at<int64_t>(g->off_core_shift)[q.core] = lds_ctl.msg_shift + D;
+                    e.template at<int64_t>(e.g->off_core_shift)[q.core] = lds_ctl.msg_shift + D;
             }
             if (D < 0) {                         // prime.cpp:130-134
                 err_or(PU_ERRF_NEG_DELAY);
@@ -2026,8 +2037,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no staging DMA outlives the wave
     if constexpr (LH) {                                   // ... and back
         __syncthreads();
-        AS1 v4u32* gh = (AS1 v4u32*)(AS1 char*)(e.base + g->off_qhdr);
-        const uint32_t nq3 = (uint32_t)g->nqueues * 3u;
+        AS1 v4u32* gh = (AS1 v4u32*)(AS1 char*)(e.base + e.g->off_qhdr);
+        const uint32_t nq3 = (uint32_t)e.g->nqueues * 3u;
         for (uint32_t k = (uint32_t)e.ln; k < nq3; k += 64) gh[(k / 3u) * PU_HDR_PIECES + k % 3u] = lds_qhdr[k];
     }
     if (e.ln == 0) {
@@ -2118,6 +2129,27 @@ __global__ __launch_bounds__(64) void unit_network_kernel(const Geo* __restrict_
 #endif
 }
 
+// M/G/1 wait (mg1_wait, queue_model_m_g_1.cpp:16-42) of many queue states at
+// once, one state per lane: the arithmetic fuzz of tests/test_gpu_mg1.py.  n is
+// the reference's UInt64 _num_arrivals, held by the engine as an exact double
+// (n < 2^53, checked by the caller).
+__global__ __launch_bounds__(256) void unit_mg1_kernel(const uint64_t* __restrict__ n, const double* __restrict__ sum,
+                                                       const double* __restrict__ sum_sq,
+                                                       const uint64_t* __restrict__ newest, uint64_t cnt,
+                                                       uint64_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cnt) return;
+    QState s;
+    s.head = 0;
+    s.count = 0;
+    s.n = (double)n[i];
+    s.sum = sum[i];
+    s.sum_sq = sum_sq[i];
+    s.newest = newest[i];
+    s.f0 = 0;
+    out[i] = mg1_wait(s);
+}
+
 // Sharer-bitmap pool: free stack [0, P) and RunState.pool_top = P per replica.
 __global__ void init_pool_kernel(char* arena, uint64_t replica_bytes, uint64_t off_pool_free, uint64_t off_run,
                                  int pool_entries, int nreplicas) {
@@ -2145,6 +2177,14 @@ extern "C" int pu_engine_init_pool(char* arena, uint64_t replica_bytes, uint64_t
 extern "C" int pu_engine_unit_queue(const Geo* d_geo, char* base, uint64_t minp, const uint64_t* t,
                                     const uint64_t* p, uint64_t n, uint64_t* out, uint64_t* mg1, hipStream_t s) {
     hipLaunchKernelGGL(unit_queue_kernel, dim3(1), dim3(64), 0, s, d_geo, base, minp, t, p, n, out, mg1);
+    return hipGetLastError() == hipSuccess ? 0 : PU_EIO;
+}
+
+extern "C" int pu_engine_unit_mg1(const uint64_t* n, const double* sum, const double* sum_sq, const uint64_t* newest,
+                                  uint64_t cnt, uint64_t* out, hipStream_t s) {
+    if (cnt == 0) return 0;
+    hipLaunchKernelGGL(unit_mg1_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, n, sum, sum_sq, newest,
+                       cnt, out);
     return hipGetLastError() == hipSuccess ? 0 : PU_EIO;
 }
 

@@ -168,7 +168,10 @@ struct EngineExec : Exec {
             hipMemcpy(d_off, full.data(), full.size() * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess)
             return pu::set_error(PU_EIO, "server: upload");
         // a negative running delay stops only that message's receive thread
-        int rc = pu::run_device_flags(h, d_reqs, d_off, d_delays, PU_KF_MSGHALT);
+        // live client timers already include the earlier replies' delays
+        // (core_manager.cpp:265): the server never applies the handle's
+        // closed-loop replay shift, whatever mode the handle was left in
+        int rc = pu::run_device_flags(h, d_reqs, d_off, d_delays, PU_KF_MSGHALT, /*use_replay_mode=*/false);
         if (!rc) rc = pu_synchronize(h);
         if (rc) return rc;
         if (hipMemcpy(delays, d_delays, n * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
@@ -376,6 +379,12 @@ int parse_conn(pu_server* s, Conn* c) {
         } else if (f.kind == kRecv) {
             Session& S = s->sess[(size_t)c->session];
             if (!S.ended) post_recv(S, c, f.tag);
+        } else if (f.kind == kSend && (f.tag < 0 || f.tag >= s->nthreads)) {
+            // prime.cpp:53: handler thread k receives tag k only, k < num_recv_threads;
+            // a message with any other tag is never received (and must not count as
+            // some thread's PROGRAM_EXITING: the engine's dead-thread mask is tag & 63)
+            std::fprintf(stderr, "[primeuncore] session %d: dropped a message with tag %d (receive threads 0..%d)\n",
+                         c->session, f.tag, s->nthreads - 1);
         } else if (f.kind == kSend) {
             Session& S = s->sess[(size_t)c->session];
             int nrec = f.a / (int)sizeof(MsgRec);

@@ -30,6 +30,7 @@
 #include "../../include/primeuncore.h"
 #include "common.h"
 #include "geometry.h"
+#include "geo_emit.h"
 
 extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,
                                 const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
@@ -39,6 +40,8 @@ extern "C" int pu_engine_init_pool(char* arena, uint64_t replica_bytes, uint64_t
                                    int pool_entries, int nreplicas, hipStream_t stream);
 extern "C" int pu_engine_unit_queue(const Geo* d_geo, char* base, uint64_t minp, const uint64_t* t,
                                     const uint64_t* p, uint64_t n, uint64_t* out, uint64_t* mg1, hipStream_t s);
+extern "C" int pu_engine_unit_mg1(const uint64_t* n, const double* sum, const double* sum_sq, const uint64_t* newest,
+                                  uint64_t cnt, uint64_t* out, hipStream_t s);
 extern "C" int pu_engine_unit_network(const Geo* d_geo, char* base, const int32_t* src, const int32_t* dst,
                                       const int32_t* len, const uint64_t* timer, uint64_t n, uint64_t* out,
                                       hipStream_t s);
@@ -380,7 +383,7 @@ int wait_stream(hipStream_t s) {
 
 int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
            hipStream_t s, uint64_t* d_pos = nullptr, uint64_t budget_ticks = 0, uint32_t extra_flags = 0,
-           bool short_launch = false) {
+           bool short_launch = false, bool use_replay_mode = true) {
     HIP_TRY(hipEventRecord(h->ev0, s), PU_EIO);
     // latency mode: with at most one replica per CU each wave keeps its queue
     // headers in the CU's LDS for the launch (engine.hip, LH). Copying the
@@ -389,7 +392,9 @@ int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const 
     // run with the headers in HBM (tools/latency_bench.py)
     const int lh = h->lds_headers_ok && nblocks <= h->cus && !short_launch ? 1 : 0;
     int rc = pu_engine_launch(h->d_geo, h->geo.num_levels, h->arena, replica0, nblocks, d_reqs, d_off, d_delay, d_pos,
-                              budget_ticks, (extra_flags & PU_KF_NOHALT) ? extra_flags : (h->replay_flags | extra_flags),
+                              budget_ticks,
+                              (extra_flags & PU_KF_NOHALT) || !use_replay_mode ? extra_flags
+                                                                               : (h->replay_flags | extra_flags),
                               lh, s);
     if (rc) return pu::set_error(rc, "engine launch failed");
     HIP_TRY(hipEventRecord(h->ev1, s), PU_EIO);
@@ -495,6 +500,19 @@ int pu_error_flags(pu_handle* h, uint64_t* out, size_t n) {
     if (n > (size_t)h->R) return pu::set_error(PU_ERANGE, "more replicas than the handle holds");
     std::lock_guard<std::mutex> lk(h->mu);
     return gather_error_flags(h, out, n);
+}
+
+long pu_config_geo_source(const pu_sim_cfg* cfg, char* buf, size_t cap) {
+    if (!cfg) return pu::set_error(PU_EINVAL, "bad arguments");
+    Geo geo;
+    if (build_geo(cfg, &geo) != 0) return PU_EINVAL;
+    const std::string s = pu::geo_cxx(geo);
+    if (buf && cap) {
+        const size_t k = s.size() < cap - 1 ? s.size() : cap - 1;
+        std::memcpy(buf, s.data(), k);
+        buf[k] = 0;
+    }
+    return (long)s.size();
 }
 
 pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device) {
@@ -723,10 +741,10 @@ int pu_run_device(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int
 }  // extern "C"
 
 int pu::run_device_flags(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
-                         uint32_t extra_flags) {
+                         uint32_t extra_flags, bool use_replay_mode) {
     if (!h || !d_reqs || !d_off || !d_delay) return pu::set_error(PU_EINVAL, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
-    return launch(h, 0, h->R, d_reqs, d_off, d_delay, h->stream, nullptr, 0, extra_flags);
+    return launch(h, 0, h->R, d_reqs, d_off, d_delay, h->stream, nullptr, 0, extra_flags, false, use_replay_mode);
 }
 
 extern "C" {
@@ -1067,6 +1085,28 @@ int pu_unit_queue_run(uint64_t min_proc, const uint64_t* t, const uint64_t* p, s
     HIP_TRY(hipDeviceSynchronize(), PU_EIO);
     if (n) HIP_TRY(hipMemcpy(delay_out, dout, n * 8, hipMemcpyDeviceToHost), PU_EIO);
     if (mg1_calls) HIP_TRY(hipMemcpy(mg1_calls, dmg, 8, hipMemcpyDeviceToHost), PU_EIO);
+    return 0;
+}
+
+int pu_unit_mg1_run(const uint64_t* num_arrivals, const double* sum, const double* sum_sq, const uint64_t* newest,
+                    size_t n, uint64_t* wait_out, int device) {
+    if ((!num_arrivals || !sum || !sum_sq || !newest || !wait_out) && n) return pu::set_error(PU_EINVAL, "bad arguments");
+    for (size_t i = 0; i < n; i++)
+        if (num_arrivals[i] >= (1ull << 53))   // the engine holds the count as an exact double
+            return pu::set_error(PU_ERANGE, "num_arrivals >= 2^53");
+    int rc = unit_prepare(device);
+    if (rc) return rc;
+    DevBufs b;
+    uint64_t* dn = b.up(num_arrivals, n);
+    double* ds = b.up(sum, n);
+    double* dq = b.up(sum_sq, n);
+    uint64_t* dw = b.up(newest, n);
+    uint64_t* dout = b.up<uint64_t>(nullptr, n);
+    if (n && (!dn || !ds || !dq || !dw || !dout)) return pu::set_error(PU_ENOMEM, "unit buffers");
+    rc = pu_engine_unit_mg1(dn, ds, dq, dw, n, dout, nullptr);
+    if (rc) return pu::set_error(rc, "unit M/G/1 launch failed");
+    HIP_TRY(hipDeviceSynchronize(), PU_EIO);
+    if (n) HIP_TRY(hipMemcpy(wait_out, dout, n * 8, hipMemcpyDeviceToHost), PU_EIO);
     return 0;
 }
 

@@ -55,6 +55,7 @@ def lib() -> C.CDLL:
         "pu_config_parse_xml": (C.c_int, [C.c_char_p, C.c_size_t, P(A.SimCfg)]),
         "pu_config_write_xml": (C.c_int, [P(A.SimCfg), C.c_char_p, C.c_size_t, P(C.c_size_t)]),
         "pu_create": (C.c_void_p, [P(A.SimCfg), C.c_int, C.c_int]),
+        "pu_config_geo_source": (C.c_long, [P(A.SimCfg), C.c_char_p, C.c_size_t]),
         "pu_destroy": (None, [C.c_void_p]),
         "pu_reset": (C.c_int, [C.c_void_p]),
         "pu_num_replicas": (C.c_int, [C.c_void_p]),
@@ -112,6 +113,8 @@ def lib() -> C.CDLL:
         "pu_client_send": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int]),
         "pu_client_recv": (C.c_int, [C.c_void_p, C.c_int, P(C.c_int32)]),
         "pu_client_close": (None, [C.c_void_p]),
+        "pu_unit_mg1_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                      C.c_int]),
         "pu_unit_queue_run": (C.c_int, [C.c_uint64, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
                                         P(C.c_uint64), C.c_int]),
         "pu_unit_network_run": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64,

@@ -305,3 +305,30 @@ def test_engine_limit_ends_session_without_reply(tmp_path):
     assert st["sessions_failed"] == 1 and st["sessions_ended"] == 1
     c.close()
     srv.close()
+
+
+def test_out_of_range_tag_is_never_received(tmp_path):
+    """prime.cpp:53: handler thread k receives tag k only (k < num_recv_threads).
+    A PROGRAM_EXITING (or any message) on another tag is dropped: it does not end
+    the session, and the session still serves its real thread afterwards."""
+    path = _sock(tmp_path)
+    srv = S.PrimeServer.with_executor(lambda s, r: _fake_delay(r), num_cores=2, socket_path=path, recv_threads=1)
+    srv.start()
+    c = S.Client(path, 0, 1)
+    c.control(MSG_PROCESS_STARTING)
+    c.control(P.uncore.MSG_NEW_THREAD, mem_size=0)
+    assert c.recv(0) == 0
+    c.control(P.uncore.MSG_PROGRAM_EXITING, tag=5)          # no receive thread 5
+    c.control(P.uncore.MSG_PROGRAM_EXITING, tag=64)         # would alias thread 0 in a 64-bit mask
+    r = np.zeros(3, P._abi.REQ_DTYPE)
+    r["timer"] = np.arange(3)
+    c.send(S.mem_message(0, r), tag=0)
+    assert c.recv(0) == int((_fake_delay(r) - 1).sum())    # the session is still live
+    assert srv.stats()["sessions_ended"] == 0
+    c.control(MSG_PROCESS_FINISHING)
+    assert c.recv(0) == 0
+    c.control(P.uncore.MSG_PROGRAM_EXITING, tag=0)
+    assert srv.join(10) == 0
+    assert srv.stats()["sessions_ended"] == 1
+    c.close()
+    srv.close()

@@ -67,3 +67,17 @@ def test_queue_model_fuzz_against_reference(seed):
     want = O.ref_queue(minp, t, p)
     got, _ = O.cpuref_queue(minp, t, p)
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref not built")
+def test_mg1_restatement_matches_reference_arithmetic():
+    """cpu_ref's mg1_wait equals the reference's own QueueModelMG1::computeQueueDelay
+    (queue_model_m_g_1.cpp:16-42, compiled in place) on 1.2M seeded states,
+    including the λ >= μ clamp and exact-integer waits (tests/mg1_states.py)."""
+    from mg1_states import states
+    n, s, q, w = states(1_200_000, seed=11)
+    want = O.ref_mg1(n, s, q, w)
+    got = O.cpuref_mg1(n, s, q, w)
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, f"{len(bad)} mismatches, first state {[x[bad[0]] for x in (n, s, q, w)]}"
+    assert (want > 0).mean() > 0.5
