@@ -238,6 +238,11 @@ int        pu_reset(pu_handle* h);
 int        pu_num_replicas(const pu_handle* h);
 /* Device bytes held by one replica's state. */
 uint64_t   pu_replica_bytes(const pu_handle* h);
+/* The share of it held by the sharer-bitmap pool (full-map sets of more than
+ * four LLCs).  pu_create sizes the pool exactly (one bitmap per directory line,
+ * up to 2 GiB) and shrinks it, with a message on stderr, only when the
+ * requested replicas would not fit the device otherwise. */
+uint64_t   pu_replica_pool_bytes(const pu_handle* h);
 /* Replicas this configuration's engine kernel keeps resident on the device at
  * once (one wave each; registers and LDS bound it).  A launch over more
  * replicas runs in several rounds.  No reference counterpart (engine sizing). */
@@ -270,6 +275,11 @@ int pu_set_replay_mode(pu_handle* h, int mode);
 
 /* PU_ERRF_* bits of replicas [0, n) (EngineStats.error_flags). */
 int pu_error_flags(pu_handle* h, uint64_t* out, size_t n);
+/* For replicas [0, n): the index, into the last launch's request array, of
+ * the first request that raised a PU_ERRF_LIMITS bit (UINT64_MAX: none).
+ * Every request before it was simulated exactly (the server still answers
+ * the messages that ended before it). */
+int pu_limit_positions(pu_handle* h, uint64_t* out, size_t n);
 
 /* Single-request compatibility path: UncoreManager::uncore_access
  * (uncore_manager.cpp:82-85).  Operates on replica 0; `*addr` is updated in
@@ -488,7 +498,8 @@ typedef int (*pu_exec_fn)(void* ctx, int session, const pu_req* reqs, size_t n, 
 /* Serve engine handle h (not owned; sessions <= pu_num_replicas(h)). */
 pu_server* pu_server_create(pu_handle* h, const pu_server_opts* o);
 pu_server* pu_server_create_exec(pu_exec_fn fn, void* ctx, int num_cores, const pu_server_opts* o);
-/* Serve until every session has ended or pu_server_stop; 0 or PU_E*. */
+/* Serve until every session has ended or pu_server_stop (which ends this run;
+ * calling pu_server_run again resumes serving); 0 or PU_E*. */
 int  pu_server_run(pu_server* s);
 /* One round, waiting up to timeout_ms for the first message; returns the
  * number of messages handled (>= 0) or PU_E*. */

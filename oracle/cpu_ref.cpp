@@ -222,6 +222,7 @@ struct Sys {
     std::vector<int64_t> core_shift;   // closed loop: the core's summed batch delays
     int64_t msg_shift = 0;             // closed loop: the open message's shift
     bool skip_msg = false;             // CPUREF_MSGHALT: the open message went negative
+    uint64_t dead_tags = 0;            // CPUREF_MSGHALT: receive threads (tag & 63) that returned
     // opt-in DRAM bank model (pu_dram_cfg): per bank the cycle it is free and
     // its open page + 1 (0 = closed)
     std::vector<int64_t> bank_ready;
@@ -901,7 +902,9 @@ long cpuref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
         const bool core_ok = q.core >= 0 && q.core < s->cores;
         if (q.batch_start) {
             delay = 0;
-            s->skip_msg = false;
+            // MSGHALT: a receive thread that returned never receives again
+            // (prime.cpp:133 returns from msgHandler; its tag = pu_req.tag)
+            s->skip_msg = msghalt && ((s->dead_tags >> (q.tag & 63)) & 1);
             if (closed && core_ok) s->msg_shift = s->core_shift[(size_t)q.core];
         }
         if (s->skip_msg) {          // MSGHALT: this message's handler thread has returned
@@ -917,6 +920,7 @@ long cpuref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
             if (closed) s->core_shift[(size_t)q.core] = s->msg_shift + delay;
         }
         if (delay < 0 && msghalt) {
+            s->dead_tags |= 1ull << (q.tag & 63);
             s->st.error_flags |= PU_ERRF_NEG_DELAY;
             s->skip_msg = true;
             continue;

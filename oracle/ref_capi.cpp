@@ -85,6 +85,7 @@ struct RefInstance {
     std::vector<int64_t> core_shift;   // closed loop: the core's summed batch delays (core_manager.cpp:265)
     int64_t msg_shift = 0;
     bool skip_msg = false;             // mode 4: the open message went negative, its rest is skipped
+    uint64_t dead_tags = 0;            // mode 4: receive threads (pu_req.tag & 63) that returned
 };
 
 static std::string slurp(const char* path) {
@@ -173,7 +174,9 @@ long ref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
         const bool core_ok = q.core >= 0 && q.core < r->num_cores;
         if (q.batch_start) {
             delay = 0;
-            r->skip_msg = false;
+            // MSGHALT: a receive thread that returned never receives again
+            // (prime.cpp:133 returns from msgHandler; its tag = pu_req.tag)
+            r->skip_msg = msghalt && ((r->dead_tags >> (q.tag & 63)) & 1);
             if (closed && core_ok) r->msg_shift = r->core_shift[(size_t)q.core];
         }
         if (r->skip_msg) {          // MSGHALT: this message's handler thread has returned
@@ -192,6 +195,7 @@ long ref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
             if (closed) r->core_shift[(size_t)q.core] = r->msg_shift + delay;
         }
         if (delay < 0 && msghalt) {
+            r->dead_tags |= 1ull << (q.tag & 63);
             r->skip_msg = true;
             continue;
         }

@@ -18,6 +18,10 @@ int set_error(int code, const std::string& msg);
 // pu_set_replay_mode left on the handle (live clients' timers are real).
 int run_device_flags(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
                      uint32_t extra_flags, bool use_replay_mode = true);
+// RunState.limit_at of replicas [0, n) after the last launch: the index into
+// that launch's request array of the first request that raised a
+// PU_ERRF_LIMITS bit (UINT64_MAX: none).
+int limit_positions(pu_handle* h, uint64_t* out, size_t n);
 
 // ThreadSched (reference src/thread_sched.cpp:55-91) with its quirks: the
 // first free core is taken, a busy core is marked with its prog id, a core is

@@ -149,6 +149,8 @@ struct LoopCtl {
     int32_t D;             // prime.cpp's running `delay` of the open message
     int32_t halted, halted0, skip;
     uint32_t flags, _pad;
+    uint64_t cur;          // index of the request being simulated
+    uint64_t limit_at;     // first request that raised a PU_ERRF_LIMITS bit (UINT64_MAX: none)
 };
 static __shared__ LoopCtl lds_ctl;
 // Engine state that only the sharer pool and the page table touch: in LDS, so
@@ -211,6 +213,12 @@ __device__ __forceinline__ void stat_add(int k, uint64_t v) {
 }
 __device__ __forceinline__ void err_or(uint64_t f) {
     lds_or_u64_lane0(lds_u32addr(&lds_err), f);
+    // rare: remember where the first engine-limit / undefined-state bit came
+    // from, so a host caller can still trust every request before it
+    if (f & PU_ERRF_LIMITS) {
+        const uint64_t cur = lds_ctl.cur;
+        if (lane_id() == 0 && cur < lds_ctl.limit_at) lds_ctl.limit_at = cur;
+    }
 }
 
 // Region cycle counters, compiled in only with -DPU_PROF (the profiling build,
@@ -1975,6 +1983,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
         lds_ctl.dead_tags = rs->dead_tags;
         lds_ctl.deadline = budget_ticks ? wave_t0 + budget_ticks : UINT64_MAX;
         lds_ctl.done = 0;
+        lds_ctl.cur = 0;
+        lds_ctl.limit_at = UINT64_MAX;
     }
     __builtin_amdgcn_wave_barrier();
     e.init_shared((int32_t)rl32(e.ln == 0 ? (uint32_t)rs->pool_top : 0u, 0), rl64(e.ln == 0 ? rs->page_next : 0ull, 0),
@@ -1991,6 +2001,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
         const pu_req q = reqs[i];
         const bool core_ok = q.core >= 0 && q.core < e.g->num_cores;
         const uint32_t fl = uni32(lds_ctl.flags);
+        if (e.ln == 0) lds_ctl.cur = i;
         if (q.batch_start && e.ln == 0) {
             lds_ctl.D = 0;
             lds_ctl.skip = (fl & PU_KF_MSGHALT) ? (int32_t)((lds_ctl.dead_tags >> (q.tag & 63)) & 1) : 0;
@@ -2048,6 +2059,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
         rs->skip_msg = lds_ctl.skip;
         rs->msg_shift = lds_ctl.msg_shift;
         rs->dead_tags = lds_ctl.dead_tags;
+        rs->limit_at = lds_ctl.limit_at;
         rs->processed += lds_ctl.done;
         rs->pool_top = lds_eng.pool_top;
         rs->page_next = lds_eng.page_next;

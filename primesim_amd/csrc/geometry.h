@@ -196,6 +196,8 @@ struct RunState {
     uint64_t last_addr;    // address of the last request after translation (InsMem::addr_dmem)
     int64_t msg_shift;     // PU_KF_CLOSED: the open message's core shift at its first request
     uint64_t dead_tags;    // PU_KF_MSGHALT: receive threads (pu_req.tag < 64) that have exited
+    uint64_t limit_at;     // last launch: index (into its request array) of the first request that
+                           // raised a PU_ERRF_LIMITS bit; UINT64_MAX if none did
 };
 static_assert(sizeof(QueueHdr) == 64, "QueueHdr is three 16-B pieces in a 64-B line");
 constexpr uint32_t PU_HDR_PIECES = (uint32_t)(sizeof(QueueHdr) / 16);   // 16-B pieces per header in HBM

@@ -130,6 +130,9 @@ struct Exec {
     virtual std::string report(int s) = 0;
     // PU_ERRF_LIMITS bits of session s after the last run (0: exact so far)
     virtual uint64_t limit_flags(int) { return 0; }
+    // index (into the last run's reqs) of the first request of session s that
+    // raised one of them: every request before it is exact.  0 = unknown.
+    virtual uint64_t limit_at(int) { return 0; }
 };
 
 // The product executor: the HIP engine, one wavefront per session.
@@ -177,12 +180,16 @@ struct EngineExec : Exec {
         if (hipMemcpy(delays, d_delays, n * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
             return pu::set_error(PU_EIO, "server: download");
         flags.assign(off.size() - 1, 0);
-        return pu_error_flags(h, flags.data(), flags.size());
+        int frc = pu_error_flags(h, flags.data(), flags.size());
+        if (frc) return frc;
+        at.assign(off.size() - 1, 0);
+        return pu::limit_positions(h, at.data(), at.size());
     }
-    std::vector<uint64_t> flags;
+    std::vector<uint64_t> flags, at;
     uint64_t limit_flags(int s) override {
         return (size_t)s < flags.size() ? flags[(size_t)s] & PU_ERRF_LIMITS : 0;
     }
+    uint64_t limit_at(int s) override { return (size_t)s < at.size() ? at[(size_t)s] : 0; }
     int alloc(int s, int p, int t) override { return pu_alloc_core_replica(h, s, p, t); }
     int dealloc(int s, int p, int t) override { return pu_dealloc_core_replica(h, s, p, t); }
     int get(int s, int p, int t) override { return pu_get_core_id_replica(h, s, p, t); }
@@ -523,9 +530,11 @@ int serve_round(pu_server* s, int timeout_ms) {
         for (const Batch& b : batches) {
             Session& S = s->sess[(size_t)b.session];
             if (S.ended) continue;
-            if (uint64_t lim = s->exec->limit_flags(b.session)) {
+            const uint64_t lim = s->exec->limit_flags(b.session);
+            if (lim && off[(size_t)b.session] + b.first + b.n > s->exec->limit_at(b.session)) {
                 // an engine limit stopped the replica where the reference continues:
-                // no reply is exact from here on, end the session with an error
+                // batches that ended before the request that hit it were answered
+                // exactly above; no reply is exact from here on: end the session
                 std::fprintf(stderr, "[primeuncore] session %d stopped by an engine limit (error flags 0x%llx)\n",
                              b.session, (unsigned long long)lim);
                 s->st.sessions_failed++;
@@ -639,6 +648,7 @@ int pu_server_round(pu_server* s, int timeout_ms) {
 
 int pu_server_run(pu_server* s) {
     if (!s) return pu::set_error(PU_EINVAL, "null server");
+    s->stop.store(false);        // pu_server_stop ends a run; a later run serves again
     while (!s->stop.load()) {
         if (s->st.sessions_ended >= s->nsessions) return 0;
         int rc = serve_round(s, 50);

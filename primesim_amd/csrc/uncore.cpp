@@ -79,7 +79,7 @@ struct Layout {
 // Validates the configuration (every condition under which the reference
 // is undefined or this engine does not implement the branch) and computes the
 // replica layout.
-int build_geo(const pu_sim_cfg* c, Geo* g) {
+int build_geo(const pu_sim_cfg* c, Geo* g, uint64_t pool_cap = 0) {
     std::memset(g, 0, sizeof(*g));
     const pu_sys_cfg& y = c->sys;
     if (y.num_levels < 1 || y.num_levels > PU_MAX_LEVELS) return pu::set_error(PU_EINVAL, "num_levels must be 1..4");
@@ -242,6 +242,7 @@ int build_geo(const pu_sim_cfg* c, Geo* g) {
         const uint64_t cap = (2ull << 30) / ((uint64_t)D.nwords * 8);
         pool = std::max<uint64_t>(std::min(dlines, cap), 64);
     }
+    if (pool_cap && !bus_sys) pool = std::max<uint64_t>(std::min(pool, pool_cap), 64);
     if (const char* e = std::getenv("PRIMEUNCORE_POOL_ENTRIES"); e && !bus_sys) pool = std::strtoull(e, nullptr, 10);
     if (pool > (1ull << 30)) pool = 1ull << 30;
     D.pool_entries = (int32_t)pool;
@@ -515,6 +516,12 @@ long pu_config_geo_source(const pu_sim_cfg* cfg, char* buf, size_t cap) {
     return (long)s.size();
 }
 
+int pu_limit_positions(pu_handle* h, uint64_t* out, size_t n) {
+    if (!h) return pu::set_error(PU_EINVAL, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    return pu::limit_positions(h, out, n);
+}
+
 pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device) {
     if (!cfg || num_replicas < 1) {
         pu::set_error(PU_EINVAL, "bad arguments");
@@ -548,6 +555,34 @@ pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device) {
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream create failed");
     if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) return fail("event create failed");
     if (hipMalloc(&h->d_geo, sizeof(Geo)) != hipSuccess) return fail("hipMalloc(geo) failed");
+    {
+        // The exact sharer pool (one bitmap per directory line, up to 2 GiB) is
+        // usually a small share of a replica, but a config whose homes see every
+        // set can make it dominate.  When the replicas asked for would not fit
+        // the device with it, shrink the pool to what fits rather than fail:
+        // running out then stops a replica loudly (PU_ERRF_POOL), never silently.
+        size_t free_b = 0, total_b = 0;
+        const uint64_t pool_b = (uint64_t)geo.dir.pool_entries * ((uint64_t)geo.dir.nwords * 8 + 4);
+        if (pool_b && hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+            geo.replica_bytes * (uint64_t)num_replicas > (uint64_t)(free_b * 0.95)) {
+            const uint64_t rest = geo.replica_bytes - pool_b;
+            const uint64_t per = (uint64_t)(free_b * 0.95) / (uint64_t)num_replicas;
+            if (per > rest + 64 * ((uint64_t)geo.dir.nwords * 8 + 4)) {
+                const uint64_t entries = (per - rest) / ((uint64_t)geo.dir.nwords * 8 + 4);
+                Geo g2;
+                if (build_geo(cfg, &g2, entries) == 0 && g2.replica_bytes < geo.replica_bytes) {
+                    std::fprintf(stderr,
+                                 "[primeuncore] sharer-bitmap pool reduced from %d to %d entries per replica so %d "
+                                 "replicas fit the device (%.1f -> %.1f MiB each); exhausting it stops a replica "
+                                 "with PU_ERRF_POOL\n",
+                                 geo.dir.pool_entries, g2.dir.pool_entries, num_replicas,
+                                 geo.replica_bytes / 1048576.0, g2.replica_bytes / 1048576.0);
+                    geo = g2;
+                    h->geo = geo;
+                }
+            }
+        }
+    }
     if (hipMemcpy(h->d_geo, &geo, sizeof(Geo), hipMemcpyHostToDevice) != hipSuccess) return fail("geo upload failed");
     size_t bytes = geo.replica_bytes * (size_t)num_replicas;
     if (hipMalloc(&h->arena, bytes) != hipSuccess) {
@@ -585,6 +620,9 @@ int pu_reset(pu_handle* h) {
 
 int pu_num_replicas(const pu_handle* h) { return h ? h->R : 0; }
 uint64_t pu_replica_bytes(const pu_handle* h) { return h ? h->geo.replica_bytes : 0; }
+uint64_t pu_replica_pool_bytes(const pu_handle* h) {
+    return h ? (uint64_t)h->geo.dir.pool_entries * ((uint64_t)h->geo.dir.nwords * 8 + 4) : 0;
+}
 
 int pu_resident_replicas(const pu_handle* h) {
     if (!h) return pu::set_error(PU_EINVAL, "null handle");
@@ -739,6 +777,17 @@ int pu_run_device(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int
 }
 
 }  // extern "C"
+
+int pu::limit_positions(pu_handle* h, uint64_t* out, size_t n) {
+    if (!h || (!out && n)) return pu::set_error(PU_EINVAL, "bad arguments");
+    if (n > (size_t)h->R) return pu::set_error(PU_ERANGE, "more replicas than the handle holds");
+    if (n == 0) return 0;
+    const Geo& g = h->geo;
+    HIP_TRY(hipStreamSynchronize(h->stream), PU_EIO);
+    HIP_TRY(hipMemcpy2D(out, sizeof(uint64_t), h->arena + g.off_run + offsetof(RunState, limit_at), g.replica_bytes,
+                        sizeof(uint64_t), n, hipMemcpyDeviceToHost), PU_EIO);
+    return 0;
+}
 
 int pu::run_device_flags(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
                          uint32_t extra_flags, bool use_replay_mode) {

@@ -60,6 +60,8 @@ def lib() -> C.CDLL:
         "pu_reset": (C.c_int, [C.c_void_p]),
         "pu_num_replicas": (C.c_int, [C.c_void_p]),
         "pu_replica_bytes": (C.c_uint64, [C.c_void_p]),
+        "pu_limit_positions": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+        "pu_replica_pool_bytes": (C.c_uint64, [C.c_void_p]),
         "pu_resident_replicas": (C.c_int, [C.c_void_p]),
         "pu_alloc_core": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
         "pu_dealloc_core": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
@@ -379,6 +381,11 @@ class UncoreManager:
         return int(lib().pu_replica_bytes(self._handle()))
 
     @property
+    def replica_pool_bytes(self) -> int:
+        """The sharer-bitmap pool's share of replica_bytes."""
+        return int(lib().pu_replica_pool_bytes(self._handle()))
+
+    @property
     def resident_replicas(self) -> int:
         """Replicas the engine kernel holds resident on the device at once."""
         n = lib().pu_resident_replicas(self._handle())
@@ -433,6 +440,15 @@ class UncoreManager:
         n = self.replicas if n is None else n
         out = np.zeros(n, dtype=np.uint64)
         if lib().pu_error_flags(self._handle(), out.ctypes.data, n) != 0:
+            raise UncoreError(last_error())
+        return out
+
+    def limit_positions(self, n: Optional[int] = None) -> np.ndarray:
+        """Per replica: index of the first request of the last launch that raised
+        a PU_ERRF_LIMITS bit (2^64-1: none)."""
+        n = self.replicas if n is None else n
+        out = np.zeros(n, dtype=np.uint64)
+        if lib().pu_limit_positions(self._handle(), out.ctypes.data, n) != 0:
             raise UncoreError(last_error())
         return out
 

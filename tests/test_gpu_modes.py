@@ -12,6 +12,7 @@
 """
 import os
 import tempfile
+import time
 
 import numpy as np
 import pytest
@@ -169,6 +170,68 @@ def test_server_stops_one_receive_thread_on_the_engine():
     dj, _ = ref.run(reqs[starts[j]:starts[j + 1]])
     assert got_j == int((dj - 1).sum())
     cl.control(P.uncore.MSG_PROGRAM_EXITING, tag=(bad_core % 2) ^ 1)   # the surviving thread returns too
+    assert srv.join(30) == 0
+    st = srv.stats()
+    assert st["sessions_halted"] == 1 and st["sessions_failed"] == 0
+    drv.close()
+    srv.close()
+    um.close()
+
+
+def test_dead_receive_thread_skips_its_later_message_in_the_same_launch():
+    """Two receive threads; the overflowing message k, a later message on the
+    SAME thread and one on the other thread are pipelined into one server round
+    (one engine launch, PU_KF_MSGHALT).  The engine abandons k, never runs the
+    dead thread's later message (its handler returned, prime.cpp:133) and answers
+    the other thread from the System k left: all as the CPU restatement's
+    MSGHALT mode with the per-thread dead mask (pinned to the reference by
+    test_modes_oracle.py) replays the same three messages."""
+    c = Case("c4_overflow_halt")
+    halt = c.meta["halt_index"]
+    sim_cfg = P.load_config(c.xml_path)
+    sim_cfg.num_recv_threads = 2
+    reqs = extended_stream(c, 36_000)
+    reqs["tag"] = reqs["core"] % 2
+    starts = np.nonzero(reqs["batch_start"])[0].tolist() + [len(reqs)]
+    k = max(i for i, st in enumerate(starts[:-1]) if st <= halt)
+    bad = int(reqs[starts[k]]["core"]) % 2
+    k2 = next(i for i in range(k + 1, len(starts) - 1) if int(reqs[starts[i]]["core"]) % 2 == bad)
+    j = next(i for i in range(k + 1, len(starts) - 1) if int(reqs[starts[i]]["core"]) % 2 != bad)
+    msgs = [reqs[starts[m]:starts[m + 1]] for m in (k, k2, j)]
+    um = P.UncoreManager()
+    um.init(sim_cfg, replicas=1)
+    path = os.path.join(tempfile.mkdtemp(prefix="pus", dir="/tmp"), "s")
+    srv = S.PrimeServer(um, path)
+    srv.start()
+    drv = S.CoreManagerDriver(path, 0, c.threads, recv_threads=2)
+    drv.start()
+    ref = O.CpuRef(sim_cfg)
+    ref.set_mode(O.MODE_MSGHALT)
+    for prog, th in c.threads:
+        ref.alloc_core(prog, th)
+    got = drv.run(reqs[:starts[k]])
+    want_d, _ = ref.run(reqs[:starts[k]])
+    assert got.tolist() == [int((want_d[a:b] - 1).sum()) for a, b in zip(starts[:k], starts[1:k + 1])]
+    srv.stop()
+    srv.join(30)
+    # the three messages are all in the server's backlog before its next round
+    for m in msgs:
+        p, t = c.threads[int(m[0]["core"])]
+        drv.clients[p].send(S.mem_message(t, m), tag=drv.tag_of[(p, t)])
+    time.sleep(0.5)                                                   # all three have arrived
+    n0, m0 = srv.stats()["launches"], srv.stats()["messages"]
+    srv.round(2000)
+    assert srv.stats()["messages"] == m0 + 3
+    assert srv.stats()["launches"] == n0 + 1                          # one launch for all three
+    srv.start()
+    pj, tj = c.threads[int(msgs[2][0]["core"])]
+    got_j = drv.clients[pj].recv(tj)
+    d3, _ = ref.run(np.concatenate(msgs))
+    na, nb = len(msgs[0]), len(msgs[1])
+    assert (d3[halt - starts[k] + 1:na + nb] == 0).all()              # k's rest and k2 never run
+    assert got_j == int((d3[na + nb:] - 1).sum())
+    pb, tb = c.threads[int(msgs[0][0]["core"])]
+    drv.clients[pb].control(P.uncore.MSG_PROGRAM_EXITING, tag=bad ^ 1)
     assert srv.join(30) == 0
     st = srv.stats()
     assert st["sessions_halted"] == 1 and st["sessions_failed"] == 0

@@ -67,6 +67,31 @@ def test_server_replays_golden(name, tmp_path):
         um.close()
 
 
+def test_server_on_a_handle_left_in_closed_mode(tmp_path):
+    """A handle switched to closed-loop replay (pu_set_replay_mode) and then
+    served: live clients' timers already include their earlier replies'
+    delays (core_manager.cpp:265), so the server's launches stay open-loop and
+    the replies are the reference's."""
+    case = Case("c1_stream")
+    um = P.UncoreManager()
+    um.init(P.load_config(case.xml_path), replicas=1)
+    um.set_replay_mode(P.uncore.PU_REPLAY_CLOSED)
+    path = _sock()
+    srv = S.PrimeServer(um, path, sessions=1)
+    try:
+        srv.start()
+        drv = S.CoreManagerDriver(path, 0, case.threads)
+        drv.start()
+        got = drv.run(case.reqs)
+        drv.finish()
+        assert srv.join(60) == 0
+        drv.close()
+        assert got.tolist() == _want(case)
+    finally:
+        srv.close()
+        um.close()
+
+
 def test_sessions_share_launches(tmp_path):
     """Three simulations on three replicas, driven concurrently: each gets the
     reference's replies, and rounds batch them into shared launches."""
@@ -163,3 +188,64 @@ def test_prime_server_executable(tmp_path):
         if proc.poll() is None:
             proc.kill()
             proc.wait()
+
+
+def test_engine_limit_mid_round_answers_the_batches_before_it(monkeypatch, tmp_path):
+    """A sharer pool of 2 entries runs out inside a round of pipelined messages
+    (c4_allcores: hotspot lines gain a fifth sharer).  Every message that ended
+    before the request that hit the limit is answered with the reference's
+    batch delay (the golden); the message holding it and everything after get
+    no reply, and the session ends as failed (limit position in
+    RunState)."""
+    c = Case("c4_allcores")
+    cfg = P.load_config(c.xml_path)
+    monkeypatch.setenv("PRIMEUNCORE_POOL_ENTRIES", "2")
+    probe = P.UncoreManager()
+    probe.init(cfg, replicas=1)
+    for prog, th in c.threads:
+        probe.allocCore(prog, th)
+    with pytest.raises(UncoreError):
+        probe.access_batch(c.reqs)
+    L = int(probe.limit_positions(1)[0])
+    probe.close()
+    starts = np.nonzero(c.reqs["batch_start"])[0].tolist() + [len(c.reqs)]
+    assert 0 < L < len(c.reqs)
+    mL = max(i for i, st in enumerate(starts[:-1]) if st <= L)
+    assert mL >= 2
+    last = min(mL + 2, len(starts) - 2)
+    um = P.UncoreManager()
+    um.init(cfg, replicas=1)
+    monkeypatch.delenv("PRIMEUNCORE_POOL_ENTRIES")
+    path = _sock()
+    srv = S.PrimeServer(um, path)
+    try:
+        srv.start()
+        drv = S.CoreManagerDriver(path, 0, c.threads)
+        drv.start()
+        srv.stop()
+        srv.join(30)
+        for m in range(last + 1):                                   # one round, one launch
+            b = c.reqs[starts[m]:starts[m + 1]]
+            p, t = c.threads[int(b[0]["core"])]
+            drv.clients[p].send(S.mem_message(t, b), tag=drv.tag_of[(p, t)])
+        time.sleep(0.5)
+        n0 = srv.stats()["launches"]
+        srv.round(2000)
+        assert srv.stats()["launches"] == n0 + 1
+        srv.start()
+        want = _want(c)
+        for m in range(mL):
+            b = c.reqs[starts[m]]
+            p, t = c.threads[int(b["core"])]
+            assert drv.clients[p].recv(t) == want[m], m
+        b = c.reqs[starts[mL]]
+        p, t = c.threads[int(b["core"])]
+        with pytest.raises(UncoreError):
+            drv.clients[p].recv(t)                                  # EOF: no exact reply exists
+        assert srv.join(30) == 0
+        st = srv.stats()
+        assert st["sessions_failed"] == 1 and st["sessions_ended"] == 1
+        drv.close()
+    finally:
+        srv.close()
+        um.close()

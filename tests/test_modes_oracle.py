@@ -16,9 +16,10 @@ from golden_util import Case, extended_stream
 
 @pytest.mark.skipif(not O.ref_available(), reason="reference not built here")
 def test_msghalt_matches_reference_past_the_overflow():
-    """A caller without prime.cpp's stop (uncore_access users, the server's
-    other receive threads): the message whose delay wraps the int is abandoned
-    at that request and the next message starts over with D = 0."""
+    """One receive thread of several (the server's PU_KF_MSGHALT): the message
+    whose delay wraps the int is abandoned at that request, its receive thread
+    (tag) never receives again, and the other thread's next message starts over
+    with D = 0 from the System the abandoned message left."""
     c = Case("c4_overflow_halt")
     halt = c.meta["halt_index"]
     ref = O.RefUncore(c.xml_path)
@@ -29,6 +30,7 @@ def test_msghalt_matches_reference_past_the_overflow():
         ref.alloc_core(prog, th)
         cpu.alloc_core(prog, th)
     reqs = extended_stream(c, 36_000)
+    reqs["tag"] = reqs["core"] % 2                     # two receive threads: tag = core % 2 (prime.cpp:105)
     want, rc = ref.run(reqs)
     assert rc == 0
     got, rc2 = cpu.run(reqs)
@@ -37,7 +39,10 @@ def test_msghalt_matches_reference_past_the_overflow():
     np.testing.assert_array_equal(want[:halt + 1], c.delays[:halt + 1])
     nxt = int(np.nonzero(reqs["batch_start"][halt + 1:])[0][0]) + halt + 1
     assert (want[halt + 1:nxt] == 0).all()             # the rest of that message is never run
-    assert (want[nxt:] != 0).all()                     # later messages are
+    dead = int(reqs["tag"][halt])
+    later = reqs[nxt:]
+    assert (want[nxt:][later["tag"] == dead] == 0).all()   # its receive thread never receives again
+    assert (want[nxt:][later["tag"] != dead] != 0).all()   # the other thread's messages are run
 
 
 def test_closed_loop_shifts_later_messages_only():
