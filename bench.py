@@ -495,6 +495,7 @@ class Device:
             self.um.allocCore(prog, th)
         self.stream = torch.cuda.Stream(self.dev)
         assert self.stream.cuda_stream != 0
+        self.compiled = P.uncore.lib().pu_compiled_config(self.um._handle()) == 1
 
     def headline(self, args, rank: int, world: int):
         import primesim_amd as P
@@ -670,6 +671,8 @@ def main(argv=None) -> None:
                 "mg1_share_of_link_visits": H.delta["mg1_calls"] / max(1, H.delta["net_distance"]),
                 "error_flags": H.errf & ~A.PU_ERRF_NEG_DELAY,
                 "engine_build": P.uncore.library_source_hash(),
+                "engine_variant": ("configuration compiled into the kernel (hipRTC, jit.cpp)" if D.compiled else
+                                   "ahead-of-time kernels (runtime geometry)"),
             },
             "per_simulation_accesses_per_s": value / tot_replicas,
             "single_instance": single,

@@ -233,6 +233,18 @@ void       pu_destroy(pu_handle* h);
  * can be specialised against (compile-time configuration).  Returns the full
  * length like snprintf; no reference counterpart. */
 long pu_config_geo_source(const pu_sim_cfg* cfg, char* buf, size_t cap);
+/* Compile-time configuration.  pu_create compiles the engine kernel for the
+ * configuration's geometry with hipRTC (every cache/mesh/latency value a
+ * constant) and launches that code object; compiled code objects are cached on
+ * disk (PRIMEUNCORE_JIT_CACHE, else jit_cache/ beside the library).
+ * PRIMEUNCORE_JIT=0, or a failed compile, runs the library's ahead-of-time
+ * kernels (the same engine source for a runtime geometry).  No reference
+ * counterpart (the reference's System reads its XmlSys at run time).
+ * pu_config_jit_warm compiles into the cache without a GPU (1: was cached,
+ * 0: compiled, PU_E* on failure); pu_compiled_config tells whether handle h
+ * runs the compiled configuration (1) or the ahead-of-time kernels (0). */
+int pu_config_jit_warm(const pu_sim_cfg* cfg);
+int pu_compiled_config(const pu_handle* h);
 /* Return all replicas to the just-initialised state (no reallocation). */
 int        pu_reset(pu_handle* h);
 int        pu_num_replicas(const pu_handle* h);

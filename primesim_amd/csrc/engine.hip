@@ -26,23 +26,27 @@
 // IEEE double in the reference's operation order; this file is compiled with
 // -ffp-contract=off so no FMA contraction changes a rounding.
 
+#ifndef __HIPCC_RTC__        // hipRTC (jit.cpp) supplies the runtime and <stdint.h> itself
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
+#ifdef __HIPCC_RTC__
+#include "primeuncore.h"      // the same file, registered under this name by jit.cpp
+#else
 #include "../../include/primeuncore.h"
+#endif
 #include "geometry.h"
 
 namespace {
 
-// Compile-time configuration: built with -DPU_JIT_GEO='"file"' (a file written
-// by pu_config_geo_source: `__device__ constexpr Geo kJitGeo = {...};`) the
-// engine kernel reads its geometry from that constant instead of the Geo
-// argument, so every configuration value folds into the code.
+// Compile-time configuration (jit.cpp): built with -DPU_JIT_GEO='"file"', a file
+// written by pu_config_geo_source (`__device__ constexpr Geo kJitGeo = {...};`
+// and `#define PU_JIT_NL <levels>`), only the kernels of that one
+// configuration are emitted and they read their geometry from the constant,
+// so every configuration value folds into the code.
 #ifdef PU_JIT_GEO
 #include PU_JIT_GEO
-#define PU_GEO(g) (&kJitGeo)
-#else
-#define PU_GEO(g) (g)
 #endif
 
 constexpr uint32_t ST_I = 0, ST_S = 1, ST_E = 2, ST_M = 3, ST_V = 4, ST_B = 5;
@@ -1940,19 +1944,18 @@ __device__ __forceinline__ void stats_init() {
 // replica of a fixed-size step.
 // SLICED is a separate instantiation so profiles list the time-sliced launches
 // (uncore_kernel<NL, true>) apart from fixed-range ones.
-template <int NL, bool SLICED, bool LH = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_MIN_WAVES(NL)))) void uncore_kernel(const Geo* __restrict__ g, char* __restrict__ arena,
-                                                    int replica0, const pu_req* __restrict__ reqs,
-                                                    const uint64_t* __restrict__ off,
-                                                    int32_t* __restrict__ delays, uint64_t* __restrict__ pos,
-                                                    uint64_t budget_ticks, uint32_t flags) {
+template <int NL, bool SLICED, bool LH>
+__device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __restrict__ arena, int replica0,
+                                            const pu_req* __restrict__ reqs, const uint64_t* __restrict__ off,
+                                            int32_t* __restrict__ delays, uint64_t* __restrict__ pos,
+                                            uint64_t budget_ticks, uint32_t flags) {
     if constexpr (!SLICED) {
         pos = nullptr;
         budget_ticks = 0;
     }
     const uint64_t wave_t0 = __builtin_amdgcn_s_memrealtime();
     Engine<NL, LH> e;
-    e.g = PU_GEO(g);
+    e.g = g;
     e.ln = lane_id();
     e.base = arena + (size_t)(replica0 + (int)blockIdx.x) * e.g->replica_bytes;
     if constexpr (LH) {                                   // the replica's queue headers into LDS
@@ -2078,6 +2081,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_
 #endif
 }
 
+#ifndef PU_JIT_GEO
+template <int NL, bool SLICED, bool LH = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_MIN_WAVES(NL)))) void uncore_kernel(
+    const Geo* __restrict__ g, char* __restrict__ arena, int replica0, const pu_req* __restrict__ reqs,
+    const uint64_t* __restrict__ off, int32_t* __restrict__ delays, uint64_t* __restrict__ pos, uint64_t budget_ticks,
+    uint32_t flags) {
+    uncore_body<NL, SLICED, LH>(g, arena, replica0, reqs, off, delays, pos, budget_ticks, flags);
+}
+#else
+}  // namespace
+// Compile-time configuration (jit.cpp): the four launch shapes of this one
+// configuration, unmangled so the host finds them by name in the code object.
+#define PU_JIT_KERNEL(NAME, S, H)                                                                                  \
+    extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H ? 1 : PU_MIN_WAVES(PU_JIT_NL)))) \
+    void NAME(const Geo* __restrict__ g, char* __restrict__ arena, int replica0, const pu_req* __restrict__ reqs,     \
+              const uint64_t* __restrict__ off, int32_t* __restrict__ delays, uint64_t* __restrict__ pos,            \
+              uint64_t budget_ticks, uint32_t flags) {                                                               \
+        uncore_body<PU_JIT_NL, S, H>(&kJitGeo, arena, replica0, reqs, off, delays, pos, budget_ticks, flags); \
+    }
+PU_JIT_KERNEL(pu_jit_uncore_s0_h0, false, false)
+PU_JIT_KERNEL(pu_jit_uncore_s0_h1, false, true)
+PU_JIT_KERNEL(pu_jit_uncore_s1_h0, true, false)
+PU_JIT_KERNEL(pu_jit_uncore_s1_h1, true, true)
+namespace {
+#endif
+
+#ifndef PU_JIT_GEO
 // Queue records start as the single free interval [0, UINT64_MAX]
 // (QueueModelHistoryTree ctor, queue_model_history_tree.cpp:28).
 __global__ void init_queues_kernel(char* arena, uint64_t replica_bytes, uint64_t off_qhdr, uint64_t off_qring,
@@ -2174,8 +2204,10 @@ __global__ void init_pool_kernel(char* arena, uint64_t replica_bytes, uint64_t o
     if (k == 0) reinterpret_cast<RunState*>(base + off_run)->pool_top = pool_entries;
 }
 
+#endif  // !PU_JIT_GEO
 }  // namespace
 
+#ifndef __HIPCC_RTC__
 extern "C" int pu_engine_init_pool(char* arena, uint64_t replica_bytes, uint64_t off_pool_free, uint64_t off_run,
                                    int pool_entries, int nreplicas, hipStream_t stream) {
     uint64_t total = (uint64_t)pool_entries * (uint64_t)nreplicas;
@@ -2286,3 +2318,4 @@ extern "C" int pu_engine_prof_blocks(unsigned long long* t0, unsigned long long*
     return n;
 }
 #endif
+#endif  // !__HIPCC_RTC__

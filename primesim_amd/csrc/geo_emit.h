@@ -21,6 +21,7 @@ inline void u(std::ostringstream& o, const char* name, uint64_t v) { o << "." <<
 inline std::string geo_cxx(const Geo& g, const char* var = "kJitGeo") {
     using namespace geo_emit_detail;
     std::ostringstream o;
+    o << "#define PU_JIT_NL " << g.num_levels << "\n";
     o << "__device__ constexpr Geo " << var << " = {";
 #define I32(x) f(o, #x, (int64_t)g.x)
 #define U64(x) u(o, #x, (uint64_t)g.x)

@@ -1,0 +1,268 @@
+// jit.cpp — compile-time configuration of the engine kernel.
+//
+// A PriME configuration (the reference's XmlSys: cache geometries, mesh,
+// latencies) is fixed for a whole simulation, so the engine kernel is compiled
+// once per configuration with every geometry value as a constant: the
+// configuration's Geo is written out as C++ (geo_emit.h), the engine's own
+// sources (embedded in this library at build time, tools/embed_src.py) are
+// compiled against it by hipRTC for gfx950, and the code object is loaded with
+// hipModuleLoadData.  Constant geometry removes the kernel's scalar loads of
+// its configuration and the scalar address arithmetic around them, the
+// largest part of the lone wave's issue and wait time.
+//
+// Code objects are cached on disk by a hash of (sources, geometry, options):
+// PRIMEUNCORE_JIT_CACHE, else jit_cache/ next to libprimeuncore.so (in-tree,
+// so a cache warmed by __graft_entry__.build() travels with the library).
+// PRIMEUNCORE_JIT=0 turns the specialisation off: the library's ahead-of-time
+// kernels (the same engine source compiled for a runtime Geo) run instead, as
+// they do when hipRTC is unavailable or a compile fails (with a message).
+#include <dlfcn.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include "common.h"
+#include "geo_emit.h"
+#include "jit.h"
+
+extern const int pu_jit_nsrc;
+extern const char* const pu_jit_src_name[];
+extern const char* const pu_jit_src_text[];
+
+namespace pu {
+namespace {
+
+// hipRTC compiles device code only and ships no C headers: the two the
+// sources include get minimal stand-ins built on the compiler's own macros.
+const char* kStdint =
+    "#pragma once\n"
+    "typedef __INT8_TYPE__ int8_t; typedef __UINT8_TYPE__ uint8_t;\n"
+    "typedef __INT16_TYPE__ int16_t; typedef __UINT16_TYPE__ uint16_t;\n"
+    "typedef __INT32_TYPE__ int32_t; typedef __UINT32_TYPE__ uint32_t;\n"
+    "typedef __INT64_TYPE__ int64_t; typedef __UINT64_TYPE__ uint64_t;\n"
+    "typedef __INTPTR_TYPE__ intptr_t; typedef __UINTPTR_TYPE__ uintptr_t;\n"
+    "#define INT64_MAX __INT64_MAX__\n#define UINT64_MAX __UINT64_MAX__\n"
+    "#define INT32_MAX __INT32_MAX__\n#define UINT32_MAX __UINT32_MAX__\n";
+const char* kStddef = "#pragma once\n";
+
+uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
+    for (unsigned char c : s) {
+        h ^= c;
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+std::string lib_dir() {
+    Dl_info info;
+    if (dladdr((void*)&fnv1a, &info) && info.dli_fname) {
+        std::string p = info.dli_fname;
+        size_t k = p.rfind('/');
+        if (k != std::string::npos) return p.substr(0, k);
+    }
+    return ".";
+}
+
+std::string cache_dir() {
+    if (const char* e = std::getenv("PRIMEUNCORE_JIT_CACHE"); e && *e) return e;
+    return lib_dir() + "/jit_cache";
+}
+
+bool read_file(const std::string& path, std::vector<char>* out) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    out->assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    return !out->empty();
+}
+
+void write_file_atomic(const std::string& path, const std::vector<char>& data) {
+    std::string tmp = path + ".tmp." + std::to_string(::getpid());
+    {
+        std::ofstream f(tmp, std::ios::binary);
+        if (!f) return;
+        f.write(data.data(), (std::streamsize)data.size());
+        if (!f) {
+            std::remove(tmp.c_str());
+            return;
+        }
+    }
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
+}
+
+std::vector<std::string> options(int waves_1level) {
+    std::vector<std::string> o = {"--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-fwrapv",
+                                  "-mllvm", "-amdgpu-sched-strategy=max-ilp", "-DPU_JIT_GEO=\"pu_jit_geo.h\"",
+                                  "-Wno-c99-designator"};
+    if (waves_1level > 0) o.push_back("-DPU_WAVES_1LEVEL=" + std::to_string(waves_1level));
+    return o;
+}
+
+int compile(const std::string& geo_src, const std::vector<std::string>& opts, std::vector<char>* code,
+            std::string* log) {
+    std::string main_src;
+    std::vector<const char*> hnames, htexts;
+    for (int i = 0; i < pu_jit_nsrc; i++) {
+        const std::string n = pu_jit_src_name[i];
+        if (n == "engine.hip") main_src = pu_jit_src_text[i];
+        else {
+            hnames.push_back(pu_jit_src_name[i]);
+            htexts.push_back(pu_jit_src_text[i]);
+        }
+    }
+    hnames.push_back("pu_jit_geo.h");
+    htexts.push_back(geo_src.c_str());
+    hnames.push_back("stdint.h");
+    htexts.push_back(kStdint);
+    hnames.push_back("stddef.h");
+    htexts.push_back(kStddef);
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, main_src.c_str(), "engine.hip", (int)hnames.size(), htexts.data(),
+                            hnames.data()) != HIPRTC_SUCCESS) {
+        *log = "hiprtcCreateProgram failed";
+        return -1;
+    }
+    std::vector<const char*> ov;
+    for (const auto& s : opts) ov.push_back(s.c_str());
+    hiprtcResult r = hiprtcCompileProgram(prog, (int)ov.size(), ov.data());
+    size_t ls = 0;
+    if (hiprtcGetProgramLogSize(prog, &ls) == HIPRTC_SUCCESS && ls > 1) {
+        log->resize(ls);
+        hiprtcGetProgramLog(prog, &(*log)[0]);
+    }
+    if (r != HIPRTC_SUCCESS) {
+        hiprtcDestroyProgram(&prog);
+        return -1;
+    }
+    size_t cs = 0;
+    hiprtcGetCodeSize(prog, &cs);
+    code->resize(cs);
+    if (cs) hiprtcGetCode(prog, code->data());
+    hiprtcDestroyProgram(&prog);
+    return cs ? 0 : -1;
+}
+
+std::mutex g_jit_mu;   // one compile at a time per process (hipRTC holds a lot of memory)
+
+}  // namespace
+
+bool jit_enabled() {
+    const char* e = std::getenv("PRIMEUNCORE_JIT");
+    return !(e && e[0] == '0');
+}
+
+std::string jit_key(const Geo& g, int waves_1level) {
+    uint64_t h = fnv1a("primeuncore-jit-1");
+    for (int i = 0; i < pu_jit_nsrc; i++) {
+        h = fnv1a(pu_jit_src_name[i], h);
+        h = fnv1a(pu_jit_src_text[i], h);
+    }
+    h = fnv1a(geo_cxx(g), h);
+    for (const auto& o : options(waves_1level)) h = fnv1a(o, h);
+    int maj = 0, min = 0;
+    hiprtcVersion(&maj, &min);
+    h = fnv1a(std::to_string(maj) + "." + std::to_string(min), h);
+    char buf[17];
+    std::snprintf(buf, sizeof buf, "%016llx", (unsigned long long)h);
+    return buf;
+}
+
+int jit_load(const Geo& g, JitKernels* out, bool verbose) {
+    *out = JitKernels{};
+    if (!jit_enabled()) return 0;
+    int waves = 0;
+    if (const char* e = std::getenv("PRIMEUNCORE_JIT_WAVES"); e && *e) waves = std::atoi(e);
+    const std::string key = jit_key(g, waves);
+    const std::string dir = cache_dir();
+    const std::string path = dir + "/" + key + ".hsaco";
+    std::vector<char> code;
+    bool cached = read_file(path, &code);
+    if (!cached) {
+        std::lock_guard<std::mutex> lk(g_jit_mu);
+        cached = read_file(path, &code);   // another thread of this process may have built it
+        if (!cached) {
+            std::string log;
+            if (verbose) std::fprintf(stderr, "[primeuncore] compiling the engine for this configuration (%s)\n", key.c_str());
+            if (compile(geo_cxx(g), options(waves), &code, &log) != 0) {
+                std::fprintf(stderr,
+                             "[primeuncore] compile-time configuration unavailable (hipRTC failed); the "
+                             "ahead-of-time kernels run instead:\n%s\n",
+                             log.c_str());
+                return 0;
+            }
+            ::mkdir(dir.c_str(), 0755);
+            write_file_atomic(path, code);
+        }
+    }
+    hipModule_t mod = nullptr;
+    if (hipModuleLoadData(&mod, code.data()) != hipSuccess) {
+        std::fprintf(stderr, "[primeuncore] could not load the configuration's code object %s; ahead-of-time "
+                             "kernels run instead\n", path.c_str());
+        return 0;
+    }
+    static const char* names[2][2] = {{"pu_jit_uncore_s0_h0", "pu_jit_uncore_s0_h1"},
+                                      {"pu_jit_uncore_s1_h0", "pu_jit_uncore_s1_h1"}};
+    for (int s = 0; s < 2; s++)
+        for (int h = 0; h < 2; h++)
+            if (hipModuleGetFunction(&out->f[s][h], mod, names[s][h]) != hipSuccess) {
+                (void)hipModuleUnload(mod);
+                *out = JitKernels{};
+                return set_error(PU_EIO, std::string("JIT code object lacks ") + names[s][h]);
+            }
+    out->mod = mod;
+    out->ok = true;
+    out->key = key;
+    return 0;
+}
+
+// Compile (or find in the cache) without loading: needs no GPU (build-time warm-up).
+int jit_warm(const Geo& g, std::string* key_out) {
+    int waves = 0;
+    if (const char* e = std::getenv("PRIMEUNCORE_JIT_WAVES"); e && *e) waves = std::atoi(e);
+    const std::string key = jit_key(g, waves);
+    if (key_out) *key_out = key;
+    const std::string dir = cache_dir();
+    const std::string path = dir + "/" + key + ".hsaco";
+    struct stat st;
+    if (::stat(path.c_str(), &st) == 0 && st.st_size > 0) return 1;
+    std::vector<char> code;
+    std::string log;
+    if (compile(geo_cxx(g), options(waves), &code, &log) != 0) return set_error(PU_EIO, "hipRTC: " + log);
+    ::mkdir(dir.c_str(), 0755);
+    write_file_atomic(path, code);
+    return 0;
+}
+
+void jit_unload(JitKernels* k) {
+    if (k->mod) (void)hipModuleUnload(k->mod);
+    *k = JitKernels{};
+}
+
+int jit_launch(const JitKernels& k, bool sliced, bool lds_headers, int nblocks, hipStream_t stream, const Geo* d_geo,
+               char* arena, int replica0, const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
+               uint64_t budget_ticks, uint32_t flags) {
+    void* args[] = {(void*)&d_geo, (void*)&arena, (void*)&replica0, (void*)&reqs, (void*)&off,
+                    (void*)&delays, (void*)&pos, (void*)&budget_ticks, (void*)&flags};
+    hipError_t e = hipModuleLaunchKernel(k.f[sliced ? 1 : 0][lds_headers ? 1 : 0], (unsigned)nblocks, 1, 1, 64, 1, 1,
+                                         0, stream, args, nullptr);
+    return e == hipSuccess ? 0 : PU_EIO;
+}
+
+int jit_occupancy(const JitKernels& k, int* blocks_per_cu) {
+    int n = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, k.f[1][0], 64, 0) != hipSuccess) return PU_EIO;
+    *blocks_per_cu = n;
+    return 0;
+}
+
+}  // namespace pu

@@ -31,6 +31,7 @@
 #include "common.h"
 #include "geometry.h"
 #include "geo_emit.h"
+#include "jit.h"
 
 extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,
                                 const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
@@ -288,6 +289,7 @@ struct pu_handle {
     int cus = 0;                 // compute units of the device (latency-mode launches)
     bool lds_headers_ok = false; // the replica's queue headers fit one CU's LDS
     bool lds_headers_short = false;   // latency mode for short host batches too
+    pu::JitKernels jit;          // the engine compiled for this configuration (jit.cpp), if available
     // ThreadSched (thread_sched.cpp): the shared one, and per-replica copies
     // made on first use of a per-replica call (pu_*_core_replica: the server's
     // sessions); the shared calls update both
@@ -392,11 +394,12 @@ int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const 
     // (a lone uncore_access, one MEM_REQUESTS message) wins back, so those
     // run with the headers in HBM (tools/latency_bench.py)
     const int lh = h->lds_headers_ok && nblocks <= h->cus && !short_launch ? 1 : 0;
-    int rc = pu_engine_launch(h->d_geo, h->geo.num_levels, h->arena, replica0, nblocks, d_reqs, d_off, d_delay, d_pos,
-                              budget_ticks,
-                              (extra_flags & PU_KF_NOHALT) || !use_replay_mode ? extra_flags
-                                                                               : (h->replay_flags | extra_flags),
-                              lh, s);
+    const uint32_t flags = (extra_flags & PU_KF_NOHALT) || !use_replay_mode ? extra_flags
+                                                                          : (h->replay_flags | extra_flags);
+    int rc = h->jit.ok ? pu::jit_launch(h->jit, d_pos != nullptr, lh != 0, nblocks, s, h->d_geo, h->arena, replica0,
+                                        d_reqs, d_off, d_delay, d_pos, budget_ticks, flags)
+                       : pu_engine_launch(h->d_geo, h->geo.num_levels, h->arena, replica0, nblocks, d_reqs, d_off,
+                                          d_delay, d_pos, budget_ticks, flags, lh, s);
     if (rc) return pu::set_error(rc, "engine launch failed");
     HIP_TRY(hipEventRecord(h->ev1, s), PU_EIO);
     return 0;
@@ -503,6 +506,15 @@ int pu_error_flags(pu_handle* h, uint64_t* out, size_t n) {
     return gather_error_flags(h, out, n);
 }
 
+int pu_config_jit_warm(const pu_sim_cfg* cfg) {
+    if (!cfg) return pu::set_error(PU_EINVAL, "bad arguments");
+    Geo geo;
+    if (build_geo(cfg, &geo) != 0) return PU_EINVAL;
+    return pu::jit_warm(geo, nullptr);
+}
+
+int pu_compiled_config(const pu_handle* h) { return h && h->jit.ok ? 1 : 0; }
+
 long pu_config_geo_source(const pu_sim_cfg* cfg, char* buf, size_t cap) {
     if (!cfg) return pu::set_error(PU_EINVAL, "bad arguments");
     Geo geo;
@@ -589,6 +601,7 @@ pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device) {
         h->arena = nullptr;
         return fail("hipMalloc of " + std::to_string(bytes) + " bytes for the replica arena failed");
     }
+    if (pu::jit_load(geo, &h->jit, true) != 0) return fail(pu::g_err);
     h->sched.stat.assign((size_t)cfg->sys.num_cores, 0);
     h->rsched.resize((size_t)num_replicas);
     if (reset_state(h) != 0) {
@@ -605,6 +618,7 @@ void pu_destroy(pu_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->arena) (void)hipFree(h->arena);
     if (h->d_geo) (void)hipFree(h->d_geo);
+    pu::jit_unload(&h->jit);
     free_stage(h);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -628,7 +642,7 @@ int pu_resident_replicas(const pu_handle* h) {
     if (!h) return pu::set_error(PU_EINVAL, "null handle");
     int per_cu = 0, cus = 0;
     HIP_TRY(hipSetDevice(h->device), PU_ENODEV);
-    int rc = pu_engine_occupancy(h->geo.num_levels, &per_cu);
+    int rc = h->jit.ok ? pu::jit_occupancy(h->jit, &per_cu) : pu_engine_occupancy(h->geo.num_levels, &per_cu);
     if (rc) return pu::set_error(rc, "occupancy query failed");
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device), PU_EIO);
     return per_cu * cus;

@@ -56,6 +56,8 @@ def lib() -> C.CDLL:
         "pu_config_write_xml": (C.c_int, [P(A.SimCfg), C.c_char_p, C.c_size_t, P(C.c_size_t)]),
         "pu_create": (C.c_void_p, [P(A.SimCfg), C.c_int, C.c_int]),
         "pu_config_geo_source": (C.c_long, [P(A.SimCfg), C.c_char_p, C.c_size_t]),
+        "pu_config_jit_warm": (C.c_int, [P(A.SimCfg)]),
+        "pu_compiled_config": (C.c_int, [C.c_void_p]),
         "pu_destroy": (None, [C.c_void_p]),
         "pu_reset": (C.c_int, [C.c_void_p]),
         "pu_num_replicas": (C.c_int, [C.c_void_p]),

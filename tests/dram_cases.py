@@ -59,3 +59,14 @@ STREAM_CASES = [
     ("c2_private_llc", "C2", {"shared_llc": 0}, A.PU_STREAM_SHARED_UNIFORM, 64, 1, 6000),
     ("c4_hotspot", "C4", {}, A.PU_STREAM_UNIFORM_HOTSPOT, 1024, 1, 20000),
 ]
+
+
+def dram_configs():
+    """(name, pu_sim_cfg) of every bank-model configuration the GPU tests build
+    (tools/jit_warm.py compiles them ahead of the GPU run)."""
+    out = [("dram one-core", one_core_config())]
+    for name, preset, over, *_ in STREAM_CASES:
+        for banks, row in ((16, 2048), (1, 64)):          # test_gpu_dram.py's two geometries
+            out.append((f"dram {name} {banks}x{row}", bank_config(preset, banks, row, **over)))
+    out.append(("dram C2 8x4096", bank_config("C2", 8, 4096)))
+    return out

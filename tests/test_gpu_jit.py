@@ -1,0 +1,38 @@
+"""The two engine variants agree with the reference: the configuration compiled
+into the kernel (jit.cpp, hipRTC; the default) and the ahead-of-time kernels
+(PRIMEUNCORE_JIT=0) that read the geometry at run time.
+
+The whole GPU suite runs the compiled configuration (pu_create's default; the
+cache is warmed by __graft_entry__.build()); here a spread of goldens (one and
+three levels, bus system, TLB, limited pointer, 3-D mesh, closed loop, a
+full-size digest) also runs on the ahead-of-time kernels, and every handle
+reports which variant it ran.
+"""
+import pytest
+
+import primesim_amd as P
+from primesim_amd import uncore
+from golden_util import Case
+from test_gpu_golden import test_engine_reproduces_reference
+
+pytestmark = pytest.mark.gpu
+
+CASES = ["c1_hot", "c3_multiprog", "three_level", "bus_c2", "tlb_c3", "limited_ptr", "mesh3d", "c4_closed",
+         "big_c4_quantum"]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_ahead_of_time_kernels_match_reference(name, monkeypatch):
+    monkeypatch.setenv("PRIMEUNCORE_JIT", "0")
+    test_engine_reproduces_reference(name)
+
+
+@pytest.mark.parametrize("jit,want", [("1", 1), ("0", 0)])
+def test_handle_reports_its_variant(jit, want, monkeypatch):
+    monkeypatch.setenv("PRIMEUNCORE_JIT", jit)
+    um = P.UncoreManager()
+    um.init(P.load_config(Case("c1_hot").xml_path), replicas=1)
+    try:
+        assert uncore.lib().pu_compiled_config(um._handle()) == want
+    finally:
+        um.close()
