@@ -161,6 +161,7 @@ def cpuref_network(nodes: int, net_type: int, data_width: int, header_flits: int
 
 
 MODE_CLOSED, MODE_NOHALT, MODE_MSGHALT = 1, 2, 4   # oracle/cpu_ref.h CPUREF_*
+MODE_MSGSKIP = 8   # abandon the rest of a message whose running delay goes negative, keep receiving
 
 
 REF_COUNTER_NAMES = ("link_visits", "link_flits", "mg1_calls", "lockdown_calls", "bus_accesses",

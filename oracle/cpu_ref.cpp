@@ -895,7 +895,10 @@ long cpuref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
         if (delays) std::fill_n(delays, n, 0);
         return n ? -1 : 0;
     }
-    const bool msghalt = (s->mode & 4) != 0;
+    // 4: one receive thread of several (the server): a negative running delay
+    // skips the rest of its message and that thread (tag) never receives again;
+    // 8: a caller of uncore_access that only abandons the message
+    const bool msghalt = (s->mode & 12) != 0, thread_dies = (s->mode & 4) != 0;
     int delay = s->batch_delay;
     for (size_t i = 0; i < n; i++) {
         const pu_req& q = reqs[i];
@@ -920,7 +923,7 @@ long cpuref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
             if (closed) s->core_shift[(size_t)q.core] = s->msg_shift + delay;
         }
         if (delay < 0 && msghalt) {
-            s->dead_tags |= 1ull << (q.tag & 63);
+            if (thread_dies) s->dead_tags |= 1ull << (q.tag & 63);
             s->st.error_flags |= PU_ERRF_NEG_DELAY;
             s->skip_msg = true;
             continue;

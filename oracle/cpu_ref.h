@@ -25,7 +25,9 @@ long cpuref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays);
  * message stop of one receive thread among several (the server). */
 #define CPUREF_CLOSED 1
 #define CPUREF_NOHALT 2
-#define CPUREF_MSGHALT 4   /* a negative running delay skips the rest of that message only */
+#define CPUREF_MSGHALT 4   /* a negative running delay skips the rest of that message, and its receive
+                              thread (pu_req.tag & 63) never receives again (the server) */
+#define CPUREF_MSGSKIP 8   /* ... skips the rest of that message only (uncore_access callers) */
 int cpuref_set_mode(void* h, int mode);
 int cpuref_stats(void* h, pu_stats* out);
 int cpuref_completion(void* h, int64_t* out, size_t n);

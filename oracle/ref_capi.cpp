@@ -165,7 +165,10 @@ long ref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
         if (delays) std::fill_n(delays, n, 0);
         return n ? -1 : 0;
     }
-    const bool msghalt = (r->mode & 4) != 0;
+    // 4: one receive thread of several (the server): a negative running delay
+    // skips the rest of its message and that thread (tag) never receives again;
+    // 8: a caller of uncore_access that only abandons the message
+    const bool msghalt = (r->mode & 12) != 0, thread_dies = (r->mode & 4) != 0;
     int delay = r->batch_delay;   // prime.cpp:113 `delay` is an int
     InsMem ins;
     std::memset(&ins, 0, sizeof(ins));
@@ -195,7 +198,7 @@ long ref_run(void* h, const pu_req* reqs, size_t n, int32_t* delays) {
             if (closed) r->core_shift[(size_t)q.core] = r->msg_shift + delay;
         }
         if (delay < 0 && msghalt) {
-            r->dead_tags |= 1ull << (q.tag & 63);
+            if (thread_dies) r->dead_tags |= 1ull << (q.tag & 63);
             r->skip_msg = true;
             continue;
         }

@@ -48,10 +48,19 @@ namespace {
 #ifdef PU_JIT_GEO
 #include PU_JIT_GEO
 #endif
+// Tool builds only (tools/build_exp.sh: profiling, experiments): the
+// ahead-of-time kernels on one configuration's constant geometry.
+#if defined(PU_FIXED_GEO) && !defined(PU_JIT_GEO)
+#include PU_FIXED_GEO
+#define PU_AOT_GEO(g) (&kJitGeo)
+#else
+#define PU_AOT_GEO(g) (g)
+#endif
 
 constexpr uint32_t ST_I = 0, ST_S = 1, ST_E = 2, ST_M = 3, ST_V = 4, ST_B = 5;
 
-__device__ __forceinline__ int lane_id() { return (int)threadIdx.x; }
+// Lane within the wavefront (latency-mode workgroups hold two waves).
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63u); }
 
 __device__ __forceinline__ uint32_t rl32(uint32_t v, int l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
@@ -62,8 +71,8 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 // lane l of v becomes x (x wave-uniform)
-__device__ __forceinline__ uint32_t wl32(uint32_t v, uint32_t x, int l) { return (int)threadIdx.x == l ? x : v; }
-__device__ __forceinline__ uint64_t wl64(uint64_t v, uint64_t x, int l) { return (int)threadIdx.x == l ? x : v; }
+__device__ __forceinline__ uint32_t wl32(uint32_t v, uint32_t x, int l) { return lane_id() == l ? x : v; }
+__device__ __forceinline__ uint64_t wl64(uint64_t v, uint64_t x, int l) { return lane_id() == l ? x : v; }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ uint32_t uni32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
@@ -410,8 +419,8 @@ __device__ __forceinline__ int lru_way(int64_t bt, int bw, uint64_t nways) {
         return (int)__builtin_amdgcn_readfirstlane(bw);
     }
     for (int o = 32; o >= 1; o >>= 1) {
-        int64_t ot = (int64_t)shfl64((uint64_t)bt, (int)threadIdx.x ^ o);
-        int ow = __shfl(bw, (int)threadIdx.x ^ o, 64);
+        int64_t ot = (int64_t)shfl64((uint64_t)bt, lane_id() ^ o);
+        int ow = __shfl(bw, lane_id() ^ o, 64);
         if (ot < bt || (ot == bt && ow < bw)) {
             bt = ot;
             bw = ow;
@@ -557,15 +566,31 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
 // Latency mode (LH): a launch with at most one replica per CU keeps every
 // queue header of its replica in the CU's LDS for the whole launch (copied in
 // at the start, back at the end), so the header round trip of each route
-// window becomes an LDS read.  136 KB: 2,176 queues (a 32x32 mesh has 1,984).
+// window becomes an LDS read.  136 KB: 2,176 queues (a 32x32 mesh has 1,984)
+// in 64-B slots: the header's three 16-B pieces a = {head, count, n},
+// b = {Σs, Σs²}, c = {newest, f0}, then d = {M/G/1 cache, unused}.
+//
+// The M/G/1 cache: the queue delay of an M/G/1 visit depends only on the
+// moments the link holds before the visit (queue_model_m_g_1.cpp:16-42), and
+// those change only when the link is visited.  In latency mode a second wave
+// of the workgroup (mg1_helper) recomputes the wait of every link a route
+// window just updated, on another SIMD, and stores it as
+// d.x = wait | (n mod 2^24) << 40; the simulating wave uses it when the tag
+// matches its header's n and computes the wait itself otherwise.  The main
+// wave writes piece a (which holds n) after b and c; the helper reads a
+// first: a wait it stores was computed from moments at least as new as its
+// tag says, so any newer moments carry another n and the tag cannot match.
 #define PU_LDS_QHDR_BYTES (136 * 1024)
+#define PU_LDS_SLOT 4u                     // 16-B pieces per LDS header slot
+#define PU_MG1_CACHE_NONE 0xFFFFFFFFFFFFFFFFull
+#define PU_MG1_WAIT_BITS 40
 #define AS3 __attribute__((address_space(3)))
 static __shared__ v4u32 lds_qhdr[PU_LDS_QHDR_BYTES / 16];
-template <bool LH>
-__device__ __forceinline__ uint32_t* hdr_ptr(const NetCtx& c, int q) {
-    if constexpr (LH) return reinterpret_cast<uint32_t*>(&lds_qhdr[(size_t)q * 3]);
-    else return (uint32_t*)(AS1 uint32_t*)q_hdr(c, q);
-}
+// queue ids whose header the main wave just wrote back, for the helper
+#define PU_HQ 256u
+static __shared__ uint16_t lds_hq[PU_HQ];
+static __shared__ uint32_t lds_hq_head;    // ids pushed so far (main writes)
+static __shared__ uint32_t lds_main_done;  // the main wave left its request loop
 
 // Header write-back of queue q by the calling lane(s).
 template <bool LH>
@@ -576,10 +601,11 @@ __device__ __forceinline__ void q_store_hdr(const NetCtx& c, int q, const QState
     const v4u32 b = v4u32{(uint32_t)sb, (uint32_t)(sb >> 32), (uint32_t)qb, (uint32_t)(qb >> 32)};
     const v4u32 cc = v4u32{(uint32_t)st.newest, (uint32_t)(st.newest >> 32), (uint32_t)st.f0, (uint32_t)(st.f0 >> 32)};
     if constexpr (LH) {
-        AS3 v4u32* H = (AS3 v4u32*)&lds_qhdr[(size_t)q * 3];
-        H[0] = a;
+        // b and c first, a (with n) last: see the M/G/1 cache above
+        volatile AS3 v4u32* H = (volatile AS3 v4u32*)&lds_qhdr[(size_t)q * PU_LDS_SLOT];
         H[1] = b;
         H[2] = cc;
+        H[0] = a;
     } else {
         AS1 uint32_t* H = q_hdr(c, q);
         *reinterpret_cast<AS1 v4u32*>(H) = a;
@@ -638,7 +664,7 @@ __device__ __forceinline__ v4u32 uni4(v4u32 v) { return v4u32{uni32(v.x), uni32(
 template <bool LH>
 __device__ __forceinline__ void hdr_load(const NetCtx& c, int q, v4u32& a, v4u32& b, v4u32& cc) {
     if constexpr (LH) {
-        const AS3 v4u32* H = (const AS3 v4u32*)&lds_qhdr[(size_t)q * 3];
+        const AS3 v4u32* H = (const AS3 v4u32*)&lds_qhdr[(size_t)q * PU_LDS_SLOT];
         a = H[0];
         b = H[1];
         cc = H[2];
@@ -785,7 +811,7 @@ static __shared__ uint32_t lds_dir_w[2][32];
 // ring head; only hops taking the tree branch fetch their full ring.
 template <bool LH>
 __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char* base_in, int src, int dst, int len,
-                                                 uint64_t timer) {
+                                                 uint64_t timer, uint32_t& hq_head) {
     PROF_T(p_pre);
     NetCtx c;
     AS1 char* base = (AS1 char*)(char*)uni64((uint64_t)base_in);
@@ -830,9 +856,11 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         const int nh = hops - b0 < 64 ? hops - b0 : 64;
         int rq = 0;
         v4u32 ha = v4u32{0, 0, 0, 0}, hb = ha, hc = ha;
+        uint64_t vcache = PU_MG1_CACHE_NONE;
         if (h < hops) {
             rq = net_route_link(c, h, sx, sy, sz, rx, ry, rz, hx, hy);
             hdr_load<LH>(c, rq, ha, hb, hc);
+            if constexpr (LH) vcache = *(const AS3 uint64_t*)&lds_qhdr[(size_t)rq * PU_LDS_SLOT + 3];
         }
         // Everything about hop h that does not depend on its arrival time is
         // computed by lane h here, once per window: the front interval (the
@@ -844,7 +872,22 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         uint32_t vhead = hs.head, vcnt = hs.count;
         uint64_t vf0 = hs.f0;
         const uint64_t vfront = vf0;    // the tree's minimum: the M/G/1 test
-        uint64_t vd = ln < nh ? mg1_wait(hs) : 0;   // hop h's queue delay if it takes M/G/1
+        // hop h's queue delay if it takes M/G/1: the helper's cached wait when
+        // its tag is this header's n, else computed here (latency mode), or
+        // computed here (throughput mode)
+        uint64_t vd = 0;
+        bool need = ln < nh;
+        if constexpr (LH) {
+            const uint64_t wmask = (1ull << PU_MG1_WAIT_BITS) - 1;
+            const bool hit = need && (vcache & wmask) != wmask && hs.n < 4294967296.0 &&
+                             (uint32_t)(vcache >> PU_MG1_WAIT_BITS) == ((uint32_t)hs.n & 0xFFFFFFu);
+            if (hit) vd = vcache & wmask;
+            need = need && !hit;
+        }
+        if (ballot(need)) {
+            const uint64_t w = mg1_wait(hs);
+            if (need) vd = w;
+        }
         uint64_t vfin = 0;              // t + d + p of hop h
         // Hop j arrives no earlier than LB_j = t + (j+1)*router + j*link_delay
         // (queue delays are >= 0).  A hop whose front free interval starts by
@@ -945,6 +988,12 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
             st.n = st.n + 1.0;
             st.newest = vfin > st.newest ? vfin : st.newest;
             q_store_hdr<LH>(c, rq, st);
+            if constexpr (LH) lds_hq[(hq_head + (uint32_t)ln) & (PU_HQ - 1)] = (uint16_t)rq;
+        }
+        if constexpr (LH) {   // publish the window's links to the helper, after their ids
+            hq_head += (uint32_t)nh;
+            asm volatile("" ::: "memory");
+            if (ln == 0) *(volatile AS3 uint32_t*)&lds_hq_head = hq_head;
         }
         // No drain here: every staged ring was waited for when its hop consumed
         // it (predicted hops are a subset of the tree hops), and the header
@@ -977,6 +1026,44 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
     return t - timer;
 }
 
+// Latency mode, the workgroup's second wave: recompute the M/G/1 wait of every
+// link the simulating wave publishes (lds_hq), from the moments in the LDS
+// header image, and store it in the link's cache slot tagged with n mod 2^24.
+// Reads piece a (n) before b and c (the main wave writes it after them).
+// Returns once the main wave has left its loop and every id is processed.
+__device__ void mg1_helper() {
+    const int ln = lane_id();
+    uint32_t tail = 0;
+    for (;;) {
+        const uint32_t head = uni32(*(volatile AS3 uint32_t*)&lds_hq_head);
+        if (head == tail) {
+            if (uni32(*(volatile AS3 uint32_t*)&lds_main_done)) {
+                if (uni32(*(volatile AS3 uint32_t*)&lds_hq_head) == tail) break;
+                continue;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        if (head - tail > PU_HQ) tail = head - PU_HQ;     // fell behind: those links just miss the cache
+        const uint32_t n = head - tail < 64u ? head - tail : 64u;
+        if ((uint32_t)ln < n) {
+            const uint32_t q = lds_hq[(tail + (uint32_t)ln) & (PU_HQ - 1)];
+            volatile AS3 v4u32* H = (volatile AS3 v4u32*)&lds_qhdr[(size_t)q * PU_LDS_SLOT];
+            const v4u32 a = H[0];
+            asm volatile("" ::: "memory");
+            const v4u32 b = H[1];
+            const v4u32 cc = H[2];
+            const QState st = hdr_state(a, b, cc);
+            const uint64_t w = mg1_wait(st);
+            const uint64_t wmask = (1ull << PU_MG1_WAIT_BITS) - 1;
+            if (w < wmask && st.n < 4294967296.0)
+                *(volatile AS3 uint64_t*)&lds_qhdr[(size_t)q * PU_LDS_SLOT + 3] =
+                    w | ((uint64_t)((uint32_t)st.n & 0xFFFFFFu) << PU_MG1_WAIT_BITS);
+        }
+        tail += n;
+    }
+}
+
 template <int NL, bool LH = false>
 struct Engine {
     const Geo* __restrict__ g;
@@ -986,6 +1073,7 @@ struct Engine {
     // reference System scratch for the requesting core (delay[core], hit_flag[core])
     int dly;
     bool hit;
+    uint32_t hq_head;   // latency mode: links published to the M/G/1 helper so far
 
     __device__ __forceinline__ void init_shared(int32_t pool_top, uint64_t page_next, uint64_t last_addr) const {
         lds_eng.pool_top = pool_top;
@@ -1016,7 +1104,7 @@ struct Engine {
     }
     __device__ __forceinline__ uint64_t transmit(int src, int dst, int len, uint64_t timer) {
         PROF_T(p0);
-        uint64_t d = net_transmit<LH>(g, base, src, dst, len, timer);
+        uint64_t d = net_transmit<LH>(g, base, src, dst, len, timer, hq_head);
         PROF_ADD(PF_NET, p0);
         return d;
     }
@@ -1958,12 +2046,30 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
     e.g = g;
     e.ln = lane_id();
     e.base = arena + (size_t)(replica0 + (int)blockIdx.x) * e.g->replica_bytes;
-    if constexpr (LH) {                                   // the replica's queue headers into LDS
-        // LDS keeps the three 16-B pieces of each header (48-B slots)
+    if constexpr (LH) {
+        // Latency mode: a two-wave workgroup.  Both waves copy the replica's
+        // queue headers into the LDS image (pieces a, b, c; d = no cached
+        // wait); wave 0 simulates, wave 1 is the M/G/1 helper (mg1_helper).
         const AS1 v4u32* gh = (const AS1 v4u32*)(AS1 char*)(e.base + e.g->off_qhdr);
-        const uint32_t nq3 = (uint32_t)e.g->nqueues * 3u;
-        for (uint32_t k = (uint32_t)e.ln; k < nq3; k += 64) lds_qhdr[k] = gh[(k / 3u) * PU_HDR_PIECES + k % 3u];
+        const uint32_t nq4 = (uint32_t)e.g->nqueues * PU_LDS_SLOT;
+        for (uint32_t k = threadIdx.x; k < nq4; k += 128)
+            lds_qhdr[k] = (k & 3u) < 3u ? gh[(k >> 2) * PU_HDR_PIECES + (k & 3u)] : v4u32{~0u, ~0u, 0u, 0u};
+        if (threadIdx.x == 0) {
+            lds_hq_head = 0;
+            lds_main_done = 0;
+        }
+        if (threadIdx.x >= 64) {                          // the helper wave
+            __syncthreads();                              // [1] stats_init's
+            mg1_helper();
+            __syncthreads();                              // [2] the main wave left its loop
+            AS1 v4u32* gho = (AS1 v4u32*)(AS1 char*)(e.base + e.g->off_qhdr);
+            for (uint32_t k = threadIdx.x; k < nq4; k += 128)
+                if ((k & 3u) < 3u) gho[(k >> 2) * PU_HDR_PIECES + (k & 3u)] = lds_qhdr[k];
+            __syncthreads();                              // [3] before the stats flush
+            return;
+        }
     }
+    e.hq_head = 0;
     stats_init();
     e.dly = 0;
     e.hit = false;
@@ -2049,11 +2155,13 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
         PROF_ADD(PF_LOOP, p_loop);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no staging DMA outlives the wave
-    if constexpr (LH) {                                   // ... and back
-        __syncthreads();
+    if constexpr (LH) {                                   // ... and the headers back
+        if (e.ln == 0) *(volatile AS3 uint32_t*)&lds_main_done = 1u;
+        __syncthreads();                                  // [2]
         AS1 v4u32* gh = (AS1 v4u32*)(AS1 char*)(e.base + e.g->off_qhdr);
-        const uint32_t nq3 = (uint32_t)e.g->nqueues * 3u;
-        for (uint32_t k = (uint32_t)e.ln; k < nq3; k += 64) gh[(k / 3u) * PU_HDR_PIECES + k % 3u] = lds_qhdr[k];
+        const uint32_t nq4 = (uint32_t)e.g->nqueues * PU_LDS_SLOT;
+        for (uint32_t k = threadIdx.x; k < nq4; k += 128)
+            if ((k & 3u) < 3u) gh[(k >> 2) * PU_HDR_PIECES + (k & 3u)] = lds_qhdr[k];
     }
     if (e.ln == 0) {
         if (pos) pos[blockIdx.x] = i;
@@ -2083,18 +2191,18 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
 
 #ifndef PU_JIT_GEO
 template <int NL, bool SLICED, bool LH = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_MIN_WAVES(NL)))) void uncore_kernel(
+__global__ __launch_bounds__(LH ? 128 : 64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_MIN_WAVES(NL)))) void uncore_kernel(
     const Geo* __restrict__ g, char* __restrict__ arena, int replica0, const pu_req* __restrict__ reqs,
     const uint64_t* __restrict__ off, int32_t* __restrict__ delays, uint64_t* __restrict__ pos, uint64_t budget_ticks,
     uint32_t flags) {
-    uncore_body<NL, SLICED, LH>(g, arena, replica0, reqs, off, delays, pos, budget_ticks, flags);
+    uncore_body<NL, SLICED, LH>(PU_AOT_GEO(g), arena, replica0, reqs, off, delays, pos, budget_ticks, flags);
 }
 #else
 }  // namespace
 // Compile-time configuration (jit.cpp): the four launch shapes of this one
 // configuration, unmangled so the host finds them by name in the code object.
 #define PU_JIT_KERNEL(NAME, S, H)                                                                                  \
-    extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H ? 1 : PU_MIN_WAVES(PU_JIT_NL)))) \
+    extern "C" __global__ __launch_bounds__(H ? 128 : 64) __attribute__((amdgpu_waves_per_eu(H ? 1 : PU_MIN_WAVES(PU_JIT_NL)))) \
     void NAME(const Geo* __restrict__ g, char* __restrict__ arena, int replica0, const pu_req* __restrict__ reqs,     \
               const uint64_t* __restrict__ off, int32_t* __restrict__ delays, uint64_t* __restrict__ pos,            \
               uint64_t budget_ticks, uint32_t flags) {                                                               \
@@ -2243,7 +2351,7 @@ extern "C" int pu_engine_unit_network(const Geo* d_geo, char* base, const int32_
 extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,
                                 const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
                                 uint64_t budget_ticks, uint32_t flags, int lds_headers, hipStream_t stream) {
-    dim3 grid((unsigned)nblocks), block(64);
+    dim3 grid((unsigned)nblocks), block(lds_headers ? 128 : 64);   // latency mode: + the M/G/1 helper wave
 #define PU_LAUNCH3(L, S, H)                                                                                        \
     hipLaunchKernelGGL((uncore_kernel<L, S, H>), grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays,   \
                        pos, budget_ticks, flags)
@@ -2280,7 +2388,7 @@ extern "C" int pu_engine_occupancy(int num_levels, int* blocks_per_cu) {
 }
 
 // Queue headers of one replica that fit the latency-mode LDS image.
-extern "C" int pu_engine_lds_header_queues(void) { return PU_LDS_QHDR_BYTES / 48; }   // 48-B LDS slots
+extern "C" int pu_engine_lds_header_queues(void) { return PU_LDS_QHDR_BYTES / (16 * PU_LDS_SLOT); }   // 64-B slots
 
 extern "C" int pu_engine_init_queues(char* arena, uint64_t replica_bytes, uint64_t off_qhdr, uint64_t off_qring,
                                      int nqueues, int nreplicas, hipStream_t stream) {

@@ -18,6 +18,7 @@
 // they do when hipRTC is unavailable or a compile fails (with a message).
 #include <dlfcn.h>
 #include <sys/stat.h>
+#include <utime.h>
 #include <unistd.h>
 
 #include <cstdio>
@@ -234,7 +235,10 @@ int jit_warm(const Geo& g, std::string* key_out) {
     const std::string dir = cache_dir();
     const std::string path = dir + "/" + key + ".hsaco";
     struct stat st;
-    if (::stat(path.c_str(), &st) == 0 && st.st_size > 0) return 1;
+    if (::stat(path.c_str(), &st) == 0 && st.st_size > 0) {
+        ::utime(path.c_str(), nullptr);   // still in use (tools/jit_warm.py prunes what is not)
+        return 1;
+    }
     std::vector<char> code;
     std::string log;
     if (compile(geo_cxx(g), options(waves), &code, &log) != 0) return set_error(PU_EIO, "hipRTC: " + log);
@@ -253,8 +257,9 @@ int jit_launch(const JitKernels& k, bool sliced, bool lds_headers, int nblocks, 
                uint64_t budget_ticks, uint32_t flags) {
     void* args[] = {(void*)&d_geo, (void*)&arena, (void*)&replica0, (void*)&reqs, (void*)&off,
                     (void*)&delays, (void*)&pos, (void*)&budget_ticks, (void*)&flags};
-    hipError_t e = hipModuleLaunchKernel(k.f[sliced ? 1 : 0][lds_headers ? 1 : 0], (unsigned)nblocks, 1, 1, 64, 1, 1,
-                                         0, stream, args, nullptr);
+    // latency mode (headers in LDS): two waves, the second the M/G/1 helper (engine.hip)
+    hipError_t e = hipModuleLaunchKernel(k.f[sliced ? 1 : 0][lds_headers ? 1 : 0], (unsigned)nblocks, 1, 1,
+                                         lds_headers ? 128 : 64, 1, 1, 0, stream, args, nullptr);
     return e == hipSuccess ? 0 : PU_EIO;
 }
 

@@ -72,14 +72,14 @@ def test_closed_loop_device_path_many_replicas():
 def test_uncore_access_does_not_halt():
     """uncore_access is System::access: no halt.  The caller runs prime.cpp's
     loop itself and, instead of exiting at the wrapped delay, abandons that
-    message and continues with the next one (CpuRef MODE_MSGHALT, pinned to the
+    message and continues with the next one (CpuRef MODE_MSGSKIP, pinned to the
     reference in test_modes_oracle.py)."""
     c = Case("c4_overflow_halt")
     halt = c.meta["halt_index"]
     cfg = P.load_config(c.xml_path)
     reqs = extended_stream(c, 36_000)
     cpu = O.CpuRef(cfg)
-    cpu.set_mode(O.MODE_MSGHALT)
+    cpu.set_mode(O.MODE_MSGSKIP)
     um = P.UncoreManager()
     um.init(cfg, replicas=1)
     for prog, th in c.threads:
@@ -137,6 +137,7 @@ def test_server_stops_one_receive_thread_on_the_engine():
     sim_cfg = P.load_config(c.xml_path)
     sim_cfg.num_recv_threads = 2
     reqs = extended_stream(c, 36_000)
+    reqs["tag"] = reqs["core"] % 2                                       # the oracle's receive threads
     starts = np.nonzero(reqs["batch_start"])[0].tolist() + [len(reqs)]
     k = max(i for i, s in enumerate(starts[:-1]) if s <= halt)          # the overflowing message
     bad_core = int(reqs[starts[k]]["core"])

@@ -45,6 +45,30 @@ def test_msghalt_matches_reference_past_the_overflow():
     assert (want[nxt:][later["tag"] != dead] != 0).all()   # the other thread's messages are run
 
 
+@pytest.mark.skipif(not O.ref_available(), reason="reference not built here")
+def test_msgskip_matches_reference_past_the_overflow():
+    """A caller of uncore_access that abandons a message whose running delay
+    wraps the int and goes on receiving (MODE_MSGSKIP): the next message starts
+    over with D = 0, on every tag."""
+    c = Case("c4_overflow_halt")
+    halt = c.meta["halt_index"]
+    ref = O.RefUncore(c.xml_path)
+    ref.set_mode(O.MODE_MSGSKIP)
+    cpu = O.CpuRef(P.load_config(c.xml_path))
+    cpu.set_mode(O.MODE_MSGSKIP)
+    for prog, th in c.threads:
+        ref.alloc_core(prog, th)
+        cpu.alloc_core(prog, th)
+    reqs = extended_stream(c, 36_000)
+    want, rc = ref.run(reqs)
+    got, rc2 = cpu.run(reqs)
+    assert rc == rc2 == 0
+    np.testing.assert_array_equal(got, want)
+    nxt = int(np.nonzero(reqs["batch_start"][halt + 1:])[0][0]) + halt + 1
+    assert (want[halt + 1:nxt] == 0).all()             # the rest of that message is never run
+    assert (want[nxt:] != 0).all()                     # later messages are, on the same tag
+
+
 def test_closed_loop_shifts_later_messages_only():
     """Closed loop leaves each core's first message untouched and shifts the
     later ones by that core's summed batch delays (host logic of the oracle)."""

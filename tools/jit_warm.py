@@ -61,7 +61,14 @@ def main() -> int:
                 print(f"[jit_warm] {name}: FAILED {err[:2000]}", flush=True)
             elif rc == 0:
                 print(f"[jit_warm] {name}: compiled in {dt:.1f}s", flush=True)
-    print(f"[jit_warm] {len(items)} configurations, {bad} failed, {time.time() - t0:.0f}s", flush=True)
+    # drop code objects no current configuration uses (older sources or geometries)
+    cache = os.environ.get("PRIMEUNCORE_JIT_CACHE") or os.path.join(ROOT, "primesim_amd", "jit_cache")
+    stale = [f for f in glob.glob(os.path.join(cache, "*.hsaco")) if os.path.getmtime(f) < t0 - 1]
+    if not bad:
+        for f in stale:
+            os.remove(f)
+    print(f"[jit_warm] {len(items)} configurations, {bad} failed, {len(stale) if not bad else 0} stale code objects "
+          f"removed, {time.time() - t0:.0f}s", flush=True)
     return 1 if bad else 0
 
 

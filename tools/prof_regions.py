@@ -16,7 +16,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PROF_LIB = os.path.join(ROOT, "primesim_amd", "libprimeuncore_prof.so")
+PROF_LIB = os.environ.get("PROF_LIB") or os.path.join(ROOT, "primesim_amd", "libprimeuncore_prof.so")
 NAMES = ["LOOP", "REQ", "NET", "NSETUP", "NHOPS", "NTREE", "NWAIT", "NWB", "SETL0", "SETLN", "HOME_LD",
          "HOME", "DOWN", "windows", "tree_hops", "demand_hops", "T_LDS", "T_SEARCH", "T_DECIDE", "T_EDIT",
          "T_STORE", "T_REFILL", "NPRE", "NPOST"]
@@ -27,6 +27,10 @@ def main() -> None:
     if not os.path.exists(PROF_LIB):
         raise SystemExit(f"{PROF_LIB} missing: make -C primesim_amd/csrc prof")
     os.environ["PRIMEUNCORE_LIB"] = PROF_LIB
+    # the region counters live in the library's own (ahead-of-time) kernels: a
+    # profiling build for one configuration's constant geometry is made with
+    # tools/build_exp.sh NAME "-DPU_PROF -DPU_FIXED_GEO=..." (PROF_LIB env)
+    os.environ["PRIMEUNCORE_JIT"] = "0"
     os.environ["PU_PROF_RESET_AFTER_WARMUP"] = "1"
     sys.path.insert(0, ROOT)
     args = [a for a in sys.argv[1:] if a != "--"]
