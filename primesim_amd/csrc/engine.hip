@@ -567,8 +567,8 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
 // queue header of its replica in the CU's LDS for the whole launch (copied in
 // at the start, back at the end), so the header round trip of each route
 // window becomes an LDS read.  136 KB: 2,176 queues (a 32x32 mesh has 1,984)
-// in 64-B slots: the header's three 16-B pieces a = {head, count, n},
-// b = {Σs, Σs²}, c = {newest, f0}, then d = {M/G/1 cache, unused}.
+// in 64-B slots: the header's three 16-B pieces a = {n, Σs},
+// b = {Σs², newest}, c = {head, count, f0}, then d = {M/G/1 cache, unused}.
 //
 // The M/G/1 cache: the queue delay of an M/G/1 visit depends only on the
 // moments the link holds before the visit (queue_model_m_g_1.cpp:16-42), and
@@ -592,25 +592,28 @@ static __shared__ uint16_t lds_hq[PU_HQ];
 static __shared__ uint32_t lds_hq_head;    // ids pushed so far (main writes)
 static __shared__ uint32_t lds_main_done;  // the main wave left its request loop
 
-// Header write-back of queue q by the calling lane(s).
+// Header write-back of queue q by the calling lane(s): pieces a = {n, Σs} and
+// b = {Σs², newest} (every visit changes them: one aligned 32-B half line),
+// and c = {head, count, f0} only when the visit changed the free-interval
+// ring (a tree visit or its prune).
 template <bool LH>
-__device__ __forceinline__ void q_store_hdr(const NetCtx& c, int q, const QState& st) {
+__device__ __forceinline__ void q_store_hdr(const NetCtx& c, int q, const QState& st, bool ring_changed = true) {
     uint64_t sb = (uint64_t)__double_as_longlong(st.sum), qb = (uint64_t)__double_as_longlong(st.sum_sq);
     const uint64_t nb = (uint64_t)__double_as_longlong(st.n);
-    const v4u32 a = v4u32{st.head, st.count, (uint32_t)nb, (uint32_t)(nb >> 32)};
-    const v4u32 b = v4u32{(uint32_t)sb, (uint32_t)(sb >> 32), (uint32_t)qb, (uint32_t)(qb >> 32)};
-    const v4u32 cc = v4u32{(uint32_t)st.newest, (uint32_t)(st.newest >> 32), (uint32_t)st.f0, (uint32_t)(st.f0 >> 32)};
+    const v4u32 a = v4u32{(uint32_t)nb, (uint32_t)(nb >> 32), (uint32_t)sb, (uint32_t)(sb >> 32)};
+    const v4u32 b = v4u32{(uint32_t)qb, (uint32_t)(qb >> 32), (uint32_t)st.newest, (uint32_t)(st.newest >> 32)};
+    const v4u32 cc = v4u32{st.head, st.count, (uint32_t)st.f0, (uint32_t)(st.f0 >> 32)};
     if constexpr (LH) {
         // b and c first, a (with n) last: see the M/G/1 cache above
         volatile AS3 v4u32* H = (volatile AS3 v4u32*)&lds_qhdr[(size_t)q * PU_LDS_SLOT];
         H[1] = b;
-        H[2] = cc;
+        if (ring_changed) H[2] = cc;
         H[0] = a;
     } else {
         AS1 uint32_t* H = q_hdr(c, q);
         *reinterpret_cast<AS1 v4u32*>(H) = a;
         *reinterpret_cast<AS1 v4u32*>(H + 4) = b;
-        *reinterpret_cast<AS1 v4u32*>(H + 8) = cc;
+        if (ring_changed) *reinterpret_cast<AS1 v4u32*>(H + 8) = cc;
     }
 }
 
@@ -651,12 +654,12 @@ __device__ __forceinline__ uint64_t q_step(const NetCtx& c, int q, QState& st, u
 __device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
 __device__ __forceinline__ QState hdr_state(v4u32 a, v4u32 b, v4u32 c) {
     QState st;
-    st.head = a.x;
-    st.count = a.y;
-    st.n = __longlong_as_double((long long)u64of(a.z, a.w));
-    st.sum = __longlong_as_double((long long)u64of(b.x, b.y));
-    st.sum_sq = __longlong_as_double((long long)u64of(b.z, b.w));
-    st.newest = u64of(c.x, c.y);
+    st.n = __longlong_as_double((long long)u64of(a.x, a.y));
+    st.sum = __longlong_as_double((long long)u64of(a.z, a.w));
+    st.sum_sq = __longlong_as_double((long long)u64of(b.x, b.y));
+    st.newest = u64of(b.z, b.w);
+    st.head = c.x;
+    st.count = c.y;
     st.f0 = u64of(c.z, c.w);
     return st;
 }
@@ -987,7 +990,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
             st.sum = st.sum + (double)plen;
             st.n = st.n + 1.0;
             st.newest = vfin > st.newest ? vfin : st.newest;
-            q_store_hdr<LH>(c, rq, st);
+            q_store_hdr<LH>(c, rq, st, vhead != hs.head || vcnt != hs.count || vf0 != hs.f0);
             if constexpr (LH) lds_hq[(hq_head + (uint32_t)ln) & (PU_HQ - 1)] = (uint16_t)rq;
         }
         if constexpr (LH) {   // publish the window's links to the helper, after their ids
@@ -1052,8 +1055,7 @@ __device__ void mg1_helper() {
             const v4u32 a = H[0];
             asm volatile("" ::: "memory");
             const v4u32 b = H[1];
-            const v4u32 cc = H[2];
-            const QState st = hdr_state(a, b, cc);
+            const QState st = hdr_state(a, b, v4u32{0u, 0u, 0u, 0u});   // M/G/1 needs a and b only
             const uint64_t w = mg1_wait(st);
             const uint64_t wmask = (1ull << PU_MG1_WAIT_BITS) - 1;
             if (w < wmask && st.n < 4294967296.0)

@@ -81,13 +81,16 @@ struct DirLine {
 // eagerly at the end of the tree op that fills it — nothing observes the tree
 // in between, and an M/G/1 visit never grows it — so the header needs the
 // tree's minimum (the M/G/1 test) but not the one after it.
+// Three 16-B pieces: a = {n, Σs} and b = {Σs², newest} change on every visit
+// (an M/G/1 visit writes back one aligned 32-B half line), c = {head, count,
+// f0} only when the visit edits the free-interval ring.
 struct QueueHdr {
-    uint32_t head;
-    uint32_t count;
     double n;          // QueueModelMG1::_num_arrivals as an exact double (< 2^53; 0.0 is all-zero bits)
     double sum;        // _sigma_service_time
     double sum_sq;     // _sigma_service_time_square
     uint64_t newest;   // _newest_arrival_time
+    uint32_t head;
+    uint32_t count;
     uint64_t f0;       // ring[head].first: the tree's minimum key (the M/G/1 test)
     uint64_t pad[2];   // one header per 64-B line: a visit reads and writes one line, not two
 };
