@@ -303,10 +303,16 @@ void end_session(pu_server* s, int si) {
     }
     // connections of an ended session get EOF (a halted or aborted handler
     // leaves its clients without replies; EOF makes that an error, not a hang)
+    // once they have collected the replies already sent to them (MPI_Send
+    // buffers them: a client receives them after the handler has returned)
     for (auto& c : s->conns)
         if (c->session == si && !c->dead) {
-            ::shutdown(c->fd, SHUT_RDWR);
-            c->dead = true;
+            bool mail = false;
+            for (const auto& kv : S.mailbox) mail |= kv.first.first == c->rank && !kv.second.empty();
+            if (!mail) {
+                ::shutdown(c->fd, SHUT_RDWR);
+                c->dead = true;
+            }
         }
 }
 
@@ -385,7 +391,19 @@ int parse_conn(pu_server* s, Conn* c) {
             return 0;
         } else if (f.kind == kRecv) {
             Session& S = s->sess[(size_t)c->session];
-            if (!S.ended) post_recv(S, c, f.tag);
+            if (!S.ended) {
+                post_recv(S, c, f.tag);
+            } else {                            // ended: hand out what was sent, then EOF
+                auto& m = S.mailbox[{c->rank, f.tag}];
+                if (!m.empty()) {
+                    reply(c, f.tag, m.front());
+                    m.pop_front();
+                } else {
+                    ::shutdown(c->fd, SHUT_RDWR);
+                    c->dead = true;
+                    return 0;
+                }
+            }
         } else if (f.kind == kSend && (f.tag < 0 || f.tag >= s->nthreads)) {
             // prime.cpp:53: handler thread k receives tag k only, k < num_recv_threads;
             // a message with any other tag is never received (and must not count as
