@@ -1266,34 +1266,38 @@ struct Engine {
 
     // ------------------------------------------------------------ sharer sets
     // Line::sharer_set (a std::set<int>, cache.h:86): up to 4 ids inline in
-    // `sh`, ascending, 16 bits each (12 bits each in the stored DirLine word);
-    // a fifth sharer moves the set to a full-map bitmap from the replica's pool
-    // (lane k holds word k).
+    // `sh`, ascending, 16 bits each (12 bits each in the stored DirLine word;
+    // above 4096 LLC nodes, DirGeo.sh_wide: 3 ids of 16 bits); one more sharer
+    // moves the set to a full-map bitmap from the replica's pool, read 64 words
+    // at a time (lane k holds word base + k).
     // the line's 10-bit program field: the id itself, or the escape for ids
     // outside [0, 1023) (their full value goes to the side array)
     static __device__ __forceinline__ uint32_t prog10(int prog) {
         return (uint32_t)prog < PU_DIR_PROG_ESC ? (uint32_t)prog : PU_DIR_PROG_ESC;
     }
-    static __device__ __forceinline__ uint64_t dir_word(uint32_t nsh, uint64_t sh, uint32_t st, uint32_t p10) {
-        const uint64_t s = nsh == PU_SH_POOL ? sh
-                         : (sh & 0xFFFull) | ((sh >> 4) & 0xFFF000ull) | ((sh >> 8) & 0xFFF000000ull) |
-                           ((sh >> 12) & 0xFFF000000000ull);
+    __device__ __forceinline__ uint64_t dir_word(uint32_t nsh, uint64_t sh, uint32_t st, uint32_t p10) const {
+        const uint64_t s = nsh == PU_SH_POOL || g->dir.sh_wide
+                               ? (sh & 0xFFFFFFFFFFFFull)
+                               : (sh & 0xFFFull) | ((sh >> 4) & 0xFFF000ull) | ((sh >> 8) & 0xFFF000000ull) |
+                                     ((sh >> 12) & 0xFFF000000000ull);
         return s | ((uint64_t)(nsh == PU_SH_POOL ? 7u : nsh) << 48) | ((uint64_t)st << 51) | ((uint64_t)p10 << 54);
     }
     static __device__ __forceinline__ uint32_t dir_state(uint64_t w) { return (uint32_t)(w >> 51) & 7u; }
-    static __device__ __forceinline__ void dir_sharers(uint64_t w, uint32_t& nsh, uint64_t& sh) {
+    __device__ __forceinline__ void dir_sharers(uint64_t w, uint32_t& nsh, uint64_t& sh) const {
         const uint32_t n = (uint32_t)(w >> 48) & 7u;
         const uint64_t s = w & 0xFFFFFFFFFFFFull;
         nsh = n == 7u ? PU_SH_POOL : n;
-        sh = n == 7u ? s
-             : (s & 0xFFFull) | ((s & 0xFFF000ull) << 4) | ((s & 0xFFF000000ull) << 8) |
-               ((s & 0xFFF000000000ull) << 12);
+        sh = n == 7u || g->dir.sh_wide
+                 ? s
+                 : (s & 0xFFFull) | ((s & 0xFFF000ull) << 4) | ((s & 0xFFF000000ull) << 8) |
+                       ((s & 0xFFF000000000ull) << 12);
     }
     __device__ __forceinline__ uint64_t* pool_of(uint64_t idx) const {
         return at<uint64_t>(g->dir.off_pool) + idx * (uint64_t)g->dir.nwords;
     }
-    __device__ __forceinline__ uint64_t pool_word(uint64_t idx) const {
-        return ln < g->dir.nwords ? pool_of(idx)[ln] : 0ull;
+    // bitmap words base .. base+63 of pool entry idx, lane k holding word base + k
+    __device__ __forceinline__ uint64_t pool_word(uint64_t idx, int base = 0) const {
+        return base + ln < g->dir.nwords ? pool_of(idx)[base + ln] : 0ull;
     }
     __device__ __forceinline__ void pool_release(uint32_t nsh, uint64_t sh) {
         if (nsh != PU_SH_POOL) return;
@@ -1315,11 +1319,13 @@ struct Engine {
     }
     __device__ int first_sharer(uint32_t nsh, uint64_t sh) {
         if (nsh == PU_SH_POOL) {
-            uint64_t w = pool_word(sh);
-            uint64_t m = ballot(w != 0);
-            if (m) {
-                int k = (int)__builtin_ctzll(m);
-                return k * 64 + (int)__builtin_ctzll(rl64(w, k));
+            for (int base = 0; base < g->dir.nwords; base += 64) {
+                uint64_t w = pool_word(sh, base);
+                uint64_t m = ballot(w != 0);
+                if (m) {
+                    int k = (int)__builtin_ctzll(m);
+                    return (base + k) * 64 + (int)__builtin_ctzll(rl64(w, k));
+                }
             }
         } else if (nsh > 0) {
             return (int)(sh & 0xFFFF);
@@ -1329,16 +1335,17 @@ struct Engine {
     }
     __device__ int count_sharers(uint32_t nsh, uint64_t sh) const {
         if (nsh != PU_SH_POOL) return (int)nsh;
-        int c = __builtin_popcountll(pool_word(sh));
+        int c = 0;
+        for (int base = 0; base < g->dir.nwords; base += 64) c += __builtin_popcountll(pool_word(sh, base));
         for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
         return (int)uni32((uint32_t)c);
     }
     // sharer_set.insert(cid)
     __device__ void add_sharer(uint32_t& nsh, uint64_t& sh, int cid) {
         if (nsh == PU_SH_POOL) {
-            if (ln == (cid >> 6)) {
-                uint64_t* P = pool_of(sh);
-                P[ln] = P[ln] | (1ull << (cid & 63));
+            if (ln == ((cid >> 6) & 63)) {
+                uint64_t* P = pool_of(sh) + (cid >> 6);
+                *P = *P | (1ull << (cid & 63));
             }
             return;
         }
@@ -1350,7 +1357,7 @@ struct Engine {
             below += id < cid;
         }
         if (present) return;
-        if (nsh < PU_SH_INLINE) {
+        if (nsh < (uint32_t)g->dir.sh_cap) {
             uint64_t low = below == 0 ? 0ull : ((1ull << (16 * below)) - 1);
             sh = (sh & low) | ((uint64_t)cid << (16 * below)) | ((sh & ~low) << 16);
             nsh++;
@@ -1358,13 +1365,15 @@ struct Engine {
         }
         uint64_t idx;
         if (!pool_alloc(&idx)) return;
-        uint64_t w = 0;
-        for (int i = 0; i < PU_SH_INLINE; i++) {
-            int id = (int)((sh >> (16 * i)) & 0xFFFF);
-            if ((id >> 6) == ln) w |= 1ull << (id & 63);
+        for (int base = 0; base < g->dir.nwords; base += 64) {
+            uint64_t w = 0;
+            for (uint32_t i = 0; i < nsh; i++) {
+                int id = (int)((sh >> (16 * i)) & 0xFFFF);
+                if ((id >> 6) == base + ln) w |= 1ull << (id & 63);
+            }
+            if ((cid >> 6) == base + ln) w |= 1ull << (cid & 63);
+            if (base + ln < g->dir.nwords) pool_of(idx)[base + ln] = w;
         }
-        if ((cid >> 6) == ln) w |= 1ull << (cid & 63);
-        if (ln < g->dir.nwords) pool_of(idx)[ln] = w;
         nsh = PU_SH_POOL;
         sh = idx;
     }
@@ -1389,7 +1398,8 @@ struct Engine {
         const bool single = mode == PR_ONE;
         const int64_t base_t = single ? timer : timer + delay;
         int pipe = single ? delay : 0, mx = 0;
-        uint64_t rem = mode == PR_POOL ? pool_word(sh) : 0ull;   // lane k: bitmap word k
+        int pbase = 0;                                            // bitmap words pbase .. pbase+63
+        uint64_t rem = mode == PR_POOL ? pool_word(sh) : 0ull;   // lane k: bitmap word pbase + k
         uint32_t k = 0;
         while (true) {
             int p;
@@ -1400,10 +1410,15 @@ struct Engine {
                 if (k >= nsh) break;
                 p = (int)((sh >> (16 * k)) & 0xFFFF);
             } else if (mode == PR_POOL) {
-                const uint64_t m = ballot(rem != 0);
+                uint64_t m = ballot(rem != 0);
+                while (!m && pbase + 64 < g->dir.nwords) {         // next 64 words (> 4096 LLC nodes)
+                    pbase += 64;
+                    rem = pool_word(sh, pbase);
+                    m = ballot(rem != 0);
+                }
                 if (!m) break;
                 const int w = (int)__builtin_ctzll(m);
-                p = w * 64 + (int)__builtin_ctzll(rl64(rem, w));
+                p = (pbase + w) * 64 + (int)__builtin_ctzll(rl64(rem, w));
                 if (ln == w) rem &= rem - 1;
             } else if (mode == PR_ALL) {
                 if ((int)k >= g->num_cores) break;

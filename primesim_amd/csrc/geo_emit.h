@@ -58,6 +58,7 @@ inline std::string geo_cxx(const Geo& g, const char* var = "kJitGeo") {
         U64(nsets); U64(nways); U64(block); U64(csets);
         I32(offbits); I32(idxbits); I32(access_time); I32(nwords);
         I32(pool_entries); I32(cset_shift);
+        I32(sh_wide); I32(sh_cap);
         U64(off_line); U64(off_pool); U64(off_pool_free); U64(off_alive); U64(off_cnt);
         U64(off_prog);
 #undef I32

@@ -38,7 +38,7 @@
 #define PU_QRING 128          // ring capacity (history tree holds <= 100 intervals)
 #define PU_QMAX 100           // QueueModelHistoryTree::_max_free_interval_size
 #define PU_MAX_WAYS 64
-#define PU_MAX_NWORDS 64      // sharer bitmap words -> up to 4096 LLC nodes
+#define PU_MAX_NWORDS 1024    // sharer bitmap words -> up to 65536 LLC nodes (16-bit inline ids)
 
 // Network geometry helpers shared by host and engine.
 static inline void pu_set_net_magic(int w, int header_flits, int data_width, int blk_len, uint64_t* w_magic,
@@ -60,8 +60,9 @@ struct LineMeta {
 
 // Directory / shared-LLC line (reference Line, cache.h:77-87, with sharer_set),
 // 24 B (measured: 32-B lines made the C4 bench 3.5% slower):
-//   w bits  0-47  sharers: up to 4 LLC ids ascending, 12 bits each (< 4096
-//                 nodes), or the pool index of a full-map bitmap
+//   w bits  0-47  sharers: up to 4 LLC ids ascending, 12 bits each (<= 4096
+//                 nodes; above: 3 ids of 16 bits, DirGeo.sh_wide), or the
+//                 pool index of a full-map bitmap
 //         bits 48-50  sharer count 0..4, 7 = pool
 //         bits 51-53  state
 //         bits 54-63  program id if 0 <= id < 1023; 1023 = escaped: the full int
@@ -133,6 +134,7 @@ struct DirGeo {
     uint64_t nsets, nways, block, csets;
     int32_t offbits, idxbits, access_time, nwords;
     int32_t pool_entries, cset_shift;
+    int32_t sh_wide, sh_cap;   // > 4096 LLC nodes: inline sharer ids are 16-bit, 3 fit (else 12-bit, 4)
     uint64_t off_line, off_pool, off_pool_free, off_alive, off_cnt;
     uint64_t off_prog;     // int32 per line: the full program id of escaped lines
 };

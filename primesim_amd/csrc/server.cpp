@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cstdint>
 #include <cstdio>
@@ -664,11 +665,39 @@ int pu_server_round(pu_server* s, int timeout_ms) {
     return serve_round(s, timeout_ms);
 }
 
+namespace {
+// A live connection of an ended session still holds replies it has not collected.
+bool undelivered(pu_server* s) {
+    for (auto& c : s->conns) {
+        if (c->dead || c->session < 0) continue;
+        const Session& S = s->sess[(size_t)c->session];
+        if (!S.ended) continue;
+        for (const auto& kv : S.mailbox)
+            if (kv.first.first == c->rank && !kv.second.empty()) return true;
+    }
+    return false;
+}
+}  // namespace
+
 int pu_server_run(pu_server* s) {
     if (!s) return pu::set_error(PU_EINVAL, "null server");
     s->stop.store(false);        // pu_server_stop ends a run; a later run serves again
+    std::chrono::steady_clock::time_point all_ended{};
     while (!s->stop.load()) {
-        if (s->st.sessions_ended >= s->nsessions) return 0;
+        if (s->st.sessions_ended >= s->nsessions) {
+            // every session has ended: keep serving receives while clients still
+            // collect replies sent before the end (for at most 10 s)
+            const auto now = std::chrono::steady_clock::now();
+            if (all_ended == std::chrono::steady_clock::time_point{}) all_ended = now;
+            if (!undelivered(s) || now - all_ended > std::chrono::seconds(10)) {
+                for (auto& c : s->conns)             // EOF for whatever a client still waits on
+                    if (!c->dead) {
+                        ::shutdown(c->fd, SHUT_RDWR);
+                        c->dead = true;
+                    }
+                return 0;
+            }
+        }
         int rc = serve_round(s, 50);
         if (rc < 0) return rc;
     }

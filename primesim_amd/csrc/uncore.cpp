@@ -139,7 +139,9 @@ int build_geo(const pu_sim_cfg* c, Geo* g, uint64_t pool_cap = 0) {
     D.idxbits = ilog2(D.nsets);
     D.access_time = dc.access_time;
     D.nwords = (N + 63) / 64;
-    if (D.nwords > PU_MAX_NWORDS) return pu::set_error(PU_ENOTSUP, "at most 4096 LLC nodes");
+    if (D.nwords > PU_MAX_NWORDS) return pu::set_error(PU_ENOTSUP, "at most 65536 LLC nodes");
+    D.sh_wide = N > 4096 ? 1 : 0;         // inline sharer ids: 4 x 12 bits, or 3 x 16 bits
+    D.sh_cap = D.sh_wide ? 3 : PU_SH_INLINE;
     if (y.protocol_type == 1 && N != y.num_cores)
         return pu::set_error(PU_EINVAL, "limited-pointer broadcast needs one LLC per core (system.cpp:623)");
     if (!bus_sys && y.network.link_delay < 1) return pu::set_error(PU_EINVAL, "link_delay must be >= 1");

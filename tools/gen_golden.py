@@ -78,6 +78,11 @@ def cases() -> dict:
     # every core active: a 20-cycle quantum gives ~8 requests per core
     c["c4_allcores"] = (CF.preset("C4"), S(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=44, quantum=20, num_quanta=2,
                                            max_requests=16000))
+    # 8192 cores (a 91x91 mesh, more than 4096 LLC nodes: 16-bit inline sharer
+    # ids, sharer bitmaps of 128 words); a 4-cycle quantum puts every core in
+    # the stream, the 64-line hotspot gives lines thousands of sharers
+    c["mesh_8192"] = (_c1_shape(8192), S(A.PU_STREAM_UNIFORM_HOTSPOT, 8192, seed=81, quantum=4, num_quanta=3,
+                                         max_requests=30000))
     c["c5_prodcons"] = (CF.preset("C5", dir_size=16384, dir_ways=4),
                         S(A.PU_STREAM_PRODUCER_CONSUMER, 4096, seed=5, quantum=8, num_quanta=2,
                           max_requests=16000))
@@ -166,7 +171,8 @@ def cases() -> dict:
 def cfg_dict(cfg: A.SimCfg) -> dict:
     def conv(o):
         if isinstance(o, (A.CacheCfg, A.NetCfg, A.SysCfg, A.SimCfg)):
-            return {k: conv(getattr(o, k)) for k, _ in o._fields_ if not k.startswith("_")}
+            # the reference's XmlSys has no <dram> (an engine-only option): not part of the fixture
+            return {k: conv(getattr(o, k)) for k, _ in o._fields_ if not k.startswith("_") and k != "dram"}
         if hasattr(o, "__len__") and not isinstance(o, (str, bytes)):
             return [conv(x) for x in o]
         return o
