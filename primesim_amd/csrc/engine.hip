@@ -239,7 +239,7 @@ __device__ __forceinline__ void err_or(uint64_t f) {
 enum ProfId {
     PF_LOOP, PF_REQ, PF_NET, PF_NSETUP, PF_NHOPS, PF_NTREE, PF_NWAIT, PF_NWB, PF_SETL0, PF_SETLN, PF_HOME_LD,
     PF_HOME, PF_DOWN, PF_WINDOWS, PF_TREEHOPS, PF_DEMAND, PF_T_LDS, PF_T_SEARCH, PF_T_DECIDE, PF_T_EDIT,
-    PF_T_STORE, PF_T_REFILL, PF_NPRE, PF_NPOST, PF_COUNT
+    PF_T_STORE, PF_T_REFILL, PF_NPRE, PF_NPOST, PF_MG1RUN, PF_MG1LANES, PF_MG1HITS, PF_MAINTAIL, PF_COUNT
 };
 #ifdef PU_PROF
 static __shared__ unsigned long long lds_prof[PF_COUNT];
@@ -888,9 +888,13 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
             need = need && !hit;
         }
         if (ballot(need)) {
+            PROF_T(p_mg1);
             const uint64_t w = mg1_wait(hs);
             if (need) vd = w;
+            PROF_ADD(PF_MG1RUN, p_mg1);
         }
+        PROF_CNT(PF_MG1LANES, (uint64_t)nh);
+        PROF_CNT(PF_MG1HITS, (uint64_t)__builtin_popcountll(ballot(ln < nh && !need)));
         uint64_t vfin = 0;              // t + d + p of hop h
         // Hop j arrives no earlier than LB_j = t + (j+1)*router + j*link_delay
         // (queue delays are >= 0).  A hop whose front free interval starts by
