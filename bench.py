@@ -685,7 +685,7 @@ def main(argv=None) -> None:
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": "uncore_kernel<1, true, false>",
+                "kernel": "pu_jit_uncore_s1_h0" if D.compiled else "uncore_kernel<1, true, false>",
                 "avg_launch_ms": avg_ms,
                 "alg_bytes_per_launch": bytes_per_launch,
                 "limiter": LIMITER,

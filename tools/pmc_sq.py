@@ -20,7 +20,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "uncore_kernel<1, true, false>"   # the timed (time-sliced, headers in HBM) launches of bench.py
+KERNEL = "pu_jit_uncore_s1_h0"   # the timed launches of bench.py (compiled configuration; AOT: "uncore_kernel<1, true, false>")
 PASSES = [
     ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"],
     ["SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_LDS", "SQ_INSTS_VALU",
@@ -52,7 +52,7 @@ def main() -> None:
                sys.executable, os.path.join(ROOT, "bench.py"), *bargs]
         print("+", " ".join(cmd), flush=True)
         with open(os.path.join(a.work, f"p{i}.log"), "w") as f:
-            r = subprocess.run(cmd, cwd=ROOT, stdout=f, stderr=subprocess.STDOUT, timeout=600)
+            r = subprocess.run(cmd, cwd=ROOT, stdout=f, stderr=subprocess.STDOUT, timeout=300)
         if r.returncode != 0:
             out[f"pass{i}_error"] = r.returncode
             continue

@@ -29,13 +29,15 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "uncore_kernel<1, true, false>"   # the timed (time-sliced, headers in HBM) launches of bench.py
+# the timed (time-sliced, headers in HBM) launches of bench.py: the compiled
+# configuration's kernel (jit.cpp) or the ahead-of-time one
+KERNELS = ("pu_jit_uncore_s1_h0", "uncore_kernel<1, true, false>")
 
 
 def run(cmd, log):
     print("+", " ".join(cmd), flush=True)
     with open(log, "w") as f:
-        r = subprocess.run(cmd, cwd=ROOT, stdout=f, stderr=subprocess.STDOUT, timeout=900)
+        r = subprocess.run(cmd, cwd=ROOT, stdout=f, stderr=subprocess.STDOUT, timeout=300)
     if r.returncode != 0:
         raise SystemExit(f"{cmd[0]} failed ({r.returncode}); see {log}")
 
@@ -51,7 +53,7 @@ def counter_rows(d):
 def per_dispatch(rows, counter):
     vals = {}
     for r in rows:
-        if KERNEL in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
+        if any(k in r.get("Kernel_Name", "") for k in KERNELS) and r.get("Counter_Name") == counter:
             did = int(r["Dispatch_Id"])
             vals[did] = vals.get(did, 0.0) + float(r["Counter_Value"])
     return [vals[k] for k in sorted(vals)]
@@ -93,7 +95,7 @@ def main():
     sys.path.insert(0, ROOT)
     from primesim_amd import uncore
     out = {
-        "kernel": KERNEL,
+        "kernel": bench_line["roofline"]["kernel"],
         "src_hash": uncore.library_source_hash(),
         "launches_measured": steps,
         "warmup": warm,
