@@ -457,6 +457,8 @@ def parse_args(argv=None):
     ap.add_argument("--single-requests", type=int, default=40960)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="headline only (profiling runs)")
+    ap.add_argument("--replay", choices=("open", "closed"), default="open",
+                    help="headline replay mode (open: the metric; closed: profiling / A/B runs of the realistic regime)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) normally; gloo for CPU-side rehearsal")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC traffic summary written by tools/pmc_traffic.py for this build")
@@ -499,7 +501,8 @@ class Device:
 
     def headline(self, args, rank: int, world: int):
         import primesim_amd as P
-        return run_pass(self.um, args, self.R, rank, world, self.dev, self.stream, P.uncore.PU_REPLAY_OPEN, args.steps,
+        mode = P.uncore.PU_REPLAY_CLOSED if args.replay == "closed" else P.uncore.PU_REPLAY_OPEN
+        return run_pass(self.um, args, self.R, rank, world, self.dev, self.stream, mode, args.steps,
                         keep_rep0=rank == 0)
 
     def reduce_device(self, args):

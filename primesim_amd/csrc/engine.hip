@@ -97,7 +97,9 @@ struct Req {
 };
 
 // A set of one cache, as held by the wave: uniform set coordinates plus the
-// lane's own way (lanes >= nways hold an invalid, never-LRU way).
+// lane's own way (lanes >= nways hold an invalid, never-LRU way).  Sets of
+// more than 64 ways are held one 64-way chunk at a time: lane w holds way
+// w0 + w (w0 = 0 for every narrower set).
 struct SetView {
     uint64_t line0;   // global line index of way 0
     uint64_t set;
@@ -106,7 +108,18 @@ struct SetView {
     int32_t mid;
     uint32_t mst;
     int64_t mts;
+    uint32_t w0;      // first way of the chunk held
 };
+
+// Sets wider than 64 ways (walked in 64-way chunks, way order) are compiled
+// into configuration-specific kernels only (jit.cpp: the geometry is a
+// constant, so narrower configurations carry none of that code); pu_create
+// refuses them for the ahead-of-time kernels.
+#if defined(PU_JIT_GEO) || defined(PU_FIXED_GEO)
+constexpr bool kWideSets = true;
+#else
+constexpr bool kWideSets = false;
+#endif
 
 // A queue's ring as held by the wave: physical slots lane and lane+64.
 struct RingView {
@@ -1123,12 +1136,19 @@ struct Engine {
         v.tag = addr >> (offbits + idxbits);
         // 32-bit index math: a level holds fewer than 2^32 lines (pu_create checks)
         v.line0 = (uint64_t)(((uint32_t)cache_index * (uint32_t)nsets + (uint32_t)v.set) * (uint32_t)nways);
-        if ((uint64_t)ln < nways) {
-            LineMeta m = meta[v.line0 + (uint64_t)ln];
+        set_chunk(v, meta, ts, nways, 0);
+    }
+    // lane w <- way w0 + w of the set
+    __device__ __forceinline__ void set_chunk(SetView& v, const LineMeta* meta, const int64_t* ts, uint64_t nways,
+                                              uint32_t w0) const {
+        v.w0 = w0;
+        const uint64_t w = (uint64_t)w0 + (uint64_t)ln;
+        if (w < nways) {
+            LineMeta m = meta[v.line0 + w];
             v.mtag = m.tag;
             v.mid = m.id;
             v.mst = m.state;
-            v.mts = ts[v.line0 + (uint64_t)ln];
+            v.mts = ts[v.line0 + w];
         } else {
             v.mtag = 0;
             v.mid = 0;
@@ -1136,29 +1156,72 @@ struct Engine {
             v.mts = INT64_MAX;
         }
     }
-    __device__ __forceinline__ int set_find(const SetView& v, uint64_t nways, int prog) const {
-        uint64_t m = ballot((uint64_t)ln < nways && v.mst != ST_I && v.mid == prog && v.mtag == v.tag);
-        return m ? (int)__builtin_ctzll(m) : -1;
+    static __device__ __forceinline__ bool wide(uint64_t nways) { return kWideSets && nways > 64; }
+    // the lane holding `way` (a way of the chunk held)
+    static __device__ __forceinline__ int wl(const SetView& v, int way) { return way - (int)v.w0; }
+    // Cache::accessLine (cache.cpp:184-202): the first matching way
+    __device__ __forceinline__ int set_find(SetView& v, const LineMeta* meta, const int64_t* ts, uint64_t nways,
+                                            int prog) const {
+        if (!wide(nways)) {
+            uint64_t m = ballot((uint64_t)ln < nways && v.mst != ST_I && v.mid == prog && v.mtag == v.tag);
+            return m ? (int)__builtin_ctzll(m) : -1;
+        }
+        for (uint32_t c = 0;; c += 64) {
+            if (c != v.w0) set_chunk(v, meta, ts, nways, c);
+            const uint64_t m =
+                ballot((uint64_t)c + (uint64_t)ln < nways && v.mst != ST_I && v.mid == prog && v.mtag == v.tag);
+            if (m) return (int)c + (int)__builtin_ctzll(m);
+            if ((uint64_t)c + 64 >= nways) return -1;
+        }
     }
     // Cache::replaceLine (cache.cpp:204-235): first invalid way, else LRU
     // (strictly smaller timestamp, lowest way on ties).  Sets tag/id only.
-    __device__ __forceinline__ int set_replace(SetView& v, LineMeta* meta, uint64_t nways, int offbits,
-                                               int idxbits, int prog, uint32_t* old_state,
+    __device__ __forceinline__ int set_replace(SetView& v, LineMeta* meta, const int64_t* ts, uint64_t nways,
+                                               int offbits, int idxbits, int prog, uint32_t* old_state,
                                                uint64_t* old_addr, int* old_prog) const {
-        uint64_t inv = ballot((uint64_t)ln < nways && v.mst == ST_I);
-        int way;
-        if (inv) {
-            way = (int)__builtin_ctzll(inv);
+        int way = -1;
+        bool invalid = false;
+        if (!wide(nways)) {
+            const uint64_t inv = ballot((uint64_t)ln < nways && v.mst == ST_I);
+            if (inv) {
+                invalid = true;
+                way = (int)__builtin_ctzll(inv);
+            } else {
+                way = lru_way(v.mts, (uint64_t)ln < nways ? ln : 64, nways);
+            }
+        } else {
+            // first invalid way over the chunks, else the (timestamp, way)
+            // minimum over them: a later chunk wins only when strictly older
+            int64_t best = INT64_MAX;
+            for (uint32_t c = 0; (uint64_t)c < nways && !invalid; c += 64) {
+                if (c != v.w0) set_chunk(v, meta, ts, nways, c);
+                const bool mine = (uint64_t)c + (uint64_t)ln < nways;
+                const uint64_t inv = ballot(mine && v.mst == ST_I);
+                if (inv) {
+                    invalid = true;
+                    way = (int)c + (int)__builtin_ctzll(inv);
+                } else {
+                    const int lw = lru_way(v.mts, mine ? ln : 64, 64);
+                    const int64_t t = (int64_t)rl64((uint64_t)v.mts, lw);
+                    if (way < 0 || t < best) {
+                        best = t;
+                        way = (int)c + lw;
+                    }
+                }
+            }
+            if ((uint32_t)way - v.w0 >= 64u) set_chunk(v, meta, ts, nways, (uint32_t)way & ~63u);
+        }
+        const int wlane = wl(v, way);
+        if (invalid) {
             *old_state = ST_I;
             *old_addr = 0;
             *old_prog = 0;
         } else {
-            way = lru_way(v.mts, (uint64_t)ln < nways ? ln : 64, nways);
-            *old_state = rl32(v.mst, way);
-            *old_addr = (v.set << offbits) | (rl64(v.mtag, way) << (offbits + idxbits));
-            *old_prog = (int)rl32((uint32_t)v.mid, way);
+            *old_state = rl32(v.mst, wlane);
+            *old_addr = (v.set << offbits) | (rl64(v.mtag, wlane) << (offbits + idxbits));
+            *old_prog = (int)rl32((uint32_t)v.mid, wlane);
         }
-        if (ln == way) {
+        if (ln == wlane) {
             v.mtag = v.tag;
             v.mid = prog;
             meta[v.line0 + (uint64_t)way] = LineMeta{v.tag, prog, v.mst};
@@ -1166,13 +1229,13 @@ struct Engine {
         return way;
     }
     __device__ __forceinline__ void set_state(SetView& v, LineMeta* meta, int way, uint32_t st) const {
-        if (ln == way) {
+        if (ln == wl(v, way)) {
             v.mst = st;
             meta[v.line0 + (uint64_t)way].state = st;
         }
     }
     __device__ __forceinline__ void set_ts(SetView& v, int64_t* ts, int way, int64_t t) const {
-        if (ln == way) {
+        if (ln == wl(v, way)) {
             v.mts = t;
             ts[v.line0 + (uint64_t)way] = t;
         }
@@ -1242,9 +1305,9 @@ struct Engine {
         if (!rl32(alive_v, cid & 63)) return 0;   // cache never created: NULL in the reference
         stat_add(SN_LOCKDOWN, 1);
         int d = L.access_time;
-        int way = set_find(v, L.nways, r.prog);
+        int way = set_find(v, at<LineMeta>(L.off_meta), at<int64_t>(L.off_ts), L.nways, r.prog);
         if (way >= 0) {
-            uint32_t st = rl32(v.mst, way);
+            uint32_t st = rl32(v.mst, wl(v, way));
             if (INVAL || st == ST_M || st == ST_E) {
                 set_state(v, at<LineMeta>(L.off_meta), way, INVAL ? ST_I : ST_S);
                 d += children<LV, INVAL>(cid, r);
@@ -1485,7 +1548,8 @@ struct Engine {
         const uint64_t set = set_index(r.addr, D.offbits, D.nsets);
         const uint64_t tag = r.addr >> (D.offbits + D.idxbits);
         const uint64_t line0 = (uint64_t)(((uint32_t)home * (uint32_t)D.csets + (uint32_t)(set >> D.cset_shift)) * (uint32_t)D.nways);
-        const bool mine = (uint64_t)ln < D.nways;
+        bool mine = (uint64_t)ln < D.nways;
+        uint32_t dw0 = 0;        // sets wider than 64 ways: lane w holds way dw0 + w
         DirLine m;
         if (staged == 1) {
             // staged before a transmit that ran hops.  With headers in HBM that
@@ -1509,7 +1573,7 @@ struct Engine {
         } else {
             m.tag = 0; m.ts = INT64_MAX; m.w = 0;
         }
-        const uint32_t m_state = dir_state(m.w);
+        uint32_t m_state = dir_state(m.w);
         // program ids: the 10-bit field decides unless either side is escaped;
         // the side array is read only then (ids >= 1023 or negative)
         const uint32_t want10 = prog10(r.prog), m_p10 = (uint32_t)(m.w >> 54);
@@ -1518,8 +1582,32 @@ struct Engine {
         if (want10 == PU_DIR_PROG_ESC || ballot(mine && m_p10 == PU_DIR_PROG_ESC)) {
             if (mine && m_p10 == PU_DIR_PROG_ESC) m_prog = side[line0 + (uint64_t)ln];
         }
-        const uint64_t hm = ballot(mine && m_state != ST_I && m_prog == r.prog && m.tag == tag);
+        // ways c..c+63 of a wide set (never staged: dir_stage takes <= 32 ways)
+        auto dir_chunk = [&](uint32_t c) {
+            dw0 = c;
+            mine = (uint64_t)c + (uint64_t)ln < D.nways;
+            if (mine) {
+                m = lines[line0 + (uint64_t)c + (uint64_t)ln];
+            } else {
+                m.tag = 0; m.ts = INT64_MAX; m.w = 0;
+            }
+            m_state = dir_state(m.w);
+            const uint32_t p10 = (uint32_t)(m.w >> 54);
+            m_prog = (int32_t)p10;
+            if (mine && p10 == PU_DIR_PROG_ESC) m_prog = side[line0 + (uint64_t)c + (uint64_t)ln];
+        };
+        uint64_t hm = ballot(mine && m_state != ST_I && m_prog == r.prog && m.tag == tag);
         int way = hm ? (int)__builtin_ctzll(hm) : -1;
+        if (wide(D.nways) && !hm) {
+            for (uint32_t c = 64; (uint64_t)c < D.nways; c += 64) {
+                dir_chunk(c);
+                hm = ballot(mine && m_state != ST_I && m_prog == r.prog && m.tag == tag);
+                if (hm) {
+                    way = (int)c + (int)__builtin_ctzll(hm);
+                    break;
+                }
+            }
+        }
         PROF_ADD(PF_HOME_LD, p_ld);
         count(D.off_cnt, home, 0);
         int delay = D.access_time;
@@ -1535,20 +1623,45 @@ struct Engine {
         bool release_set = false, miss_fill = false;
         if (way < 0 && r.type != PU_WB) {
             // replaceLine (cache.cpp:204-235): first invalid way, else LRU
-            const uint64_t inv = ballot(mine && m_state == ST_I);
             uint32_t old_st = ST_I;
             uint64_t old_addr = 0;
             int old_prog = 0;
-            if (inv) {
-                way = (int)__builtin_ctzll(inv);
+            bool inv = false;
+            if (!wide(D.nways)) {
+                const uint64_t im = ballot(mine && m_state == ST_I);
+                inv = im != 0;
+                if (inv) {
+                    way = (int)__builtin_ctzll(im);
+                } else {
+                    way = lru_way(m.ts, mine ? ln : 64, D.nways);
+                }
             } else {
-                way = lru_way(m.ts, mine ? ln : 64, D.nways);
+                // first invalid way over the chunks, else the (timestamp, way)
+                // minimum (a later chunk wins only when strictly older)
+                int64_t best = INT64_MAX;
+                for (uint32_t c = 0; (uint64_t)c < D.nways && !inv; c += 64) {
+                    if (c != dw0) dir_chunk(c);
+                    const uint64_t im = ballot(mine && m_state == ST_I);
+                    if (im) {
+                        inv = true;
+                        way = (int)c + (int)__builtin_ctzll(im);
+                    } else {
+                        const int lw = lru_way(m.ts, mine ? ln : 64, 64);
+                        const int64_t t = (int64_t)rl64((uint64_t)m.ts, lw);
+                        if (way < 0 || t < best) {
+                            best = t;
+                            way = (int)c + lw;
+                        }
+                    }
+                }
+                if ((uint32_t)way - dw0 >= 64u) dir_chunk((uint32_t)way & ~63u);
             }
-            const uint64_t ww = rl64(m.w, way);
+            const int wlane = way - (int)dw0;
+            const uint64_t ww = rl64(m.w, wlane);
             if (!inv) {
                 old_st = dir_state(ww);
-                old_addr = (set << D.offbits) | (rl64(m.tag, way) << (D.offbits + D.idxbits));
-                old_prog = (int)rl32((uint32_t)m_prog, way);
+                old_addr = (set << D.offbits) | (rl64(m.tag, wlane) << (D.offbits + D.idxbits));
+                old_prog = (int)rl32((uint32_t)m_prog, wlane);
             }
             dir_sharers(ww, nsh, sh);
             if (old_st != ST_I) {
@@ -1574,7 +1687,7 @@ struct Engine {
             *out_state = ST_I;
             return delay;
         } else {
-            const uint64_t ww = rl64(m.w, way);
+            const uint64_t ww = rl64(m.w, way - (int)dw0);
             st = dir_state(ww);
             dir_sharers(ww, nsh, sh);
             if (r.type == PU_WR) {
@@ -1632,7 +1745,7 @@ struct Engine {
             add_sharer(nsh, sh, cid);
         }
         *out_state = st == ST_B ? ST_S : st;
-        if (ln == way) {
+        if (ln == way - (int)dw0) {
             // home slices stamp the arrival time (Q4)
             lines[line0 + (uint64_t)way] = DirLine{tag, timer, dir_word(nsh, sh, st, want10)};
             if (want10 == PU_DIR_PROG_ESC) side[line0 + (uint64_t)way] = r.prog;
@@ -1673,7 +1786,7 @@ struct Engine {
         }
         if (!hit) count(L.off_cnt, cid, 0);
         dly += L.access_time;
-        int way = set_find(v, L.nways, r.prog);
+        int way = set_find(v, meta, tsa, L.nways, r.prog);
         PROF_ADD(LV == 0 ? PF_SETL0 : PF_SETLN, p_set);
         bool is_miss = false, call_parent = false;
         int64_t ptimer = 0;
@@ -1686,7 +1799,7 @@ struct Engine {
         if (way >= 0) {                                      // hit
             set_ts(v, tsa, way, timer + dly);
             hit = true;
-            const uint32_t st = rl32(v.mst, way);
+            const uint32_t st = rl32(v.mst, wl(v, way));
             if (r.type == PU_WR) {
                 if constexpr (!kLast) {
                     if (st != ST_M) {
@@ -1710,7 +1823,7 @@ struct Engine {
             uint32_t old_st;
             uint64_t old_addr;
             int old_prog;
-            way = set_replace(v, meta, L.nways, L.offbits, L.idxbits, r.prog, &old_st, &old_addr, &old_prog);
+            way = set_replace(v, meta, tsa, L.nways, L.offbits, L.idxbits, r.prog, &old_st, &old_addr, &old_prog);
             if (old_st != ST_I) {
                 count(L.off_cnt, cid, 2);
                 Req o{old_addr, old_prog, PU_RD};
@@ -1846,14 +1959,14 @@ struct Engine {
         }
         dly += L.access_time;
         if (!hit) count(L.off_cnt, cid, 0);
-        int way = set_find(v, L.nways, r.prog);
+        int way = set_find(v, meta, tsa, L.nways, r.prog);
         bool is_miss = false, call_parent = false;
         int snoop_mode = -1;
         uint32_t ret = ST_M;
         if (way >= 0) {                                      // hit
             set_ts(v, tsa, way, timer + dly);
             hit = true;
-            const uint32_t st = rl32(v.mst, way);
+            const uint32_t st = rl32(v.mst, wl(v, way));
             if (r.type != PU_WR) {
                 if (st != ST_S) children<LV, false>(cid, r);   // share_children, delay discarded
                 return ST_S;
@@ -1871,7 +1984,7 @@ struct Engine {
             uint32_t old_st;
             uint64_t old_addr;
             int old_prog;
-            way = set_replace(v, meta, L.nways, L.offbits, L.idxbits, r.prog, &old_st, &old_addr, &old_prog);
+            way = set_replace(v, meta, tsa, L.nways, L.offbits, L.idxbits, r.prog, &old_st, &old_addr, &old_prog);
             if (old_st != ST_I) {
                 Req o{old_addr, old_prog, PU_RD};
                 children<LV, true>(cid, o);                  // inval_children, delay discarded
@@ -1955,22 +2068,24 @@ struct Engine {
         uint64_t* ppa = at<uint64_t>(T.off_ppage);
         SetView v;
         set_load(v, meta, tsa, T.nsets, T.nways, T.offbits, T.idxbits, (uint64_t)core, r.addr);
-        const uint64_t mypp = (uint64_t)ln < T.nways ? ppa[v.line0 + (uint64_t)ln] : 0ull;
+        const uint64_t mypp = !wide(T.nways) && (uint64_t)ln < T.nways ? ppa[v.line0 + (uint64_t)ln] : 0ull;
         count(T.off_cnt, core, 0);
         int d = T.access_time;
-        int way = set_find(v, T.nways, r.prog);
+        int way = set_find(v, meta, tsa, T.nways, r.prog);
         uint64_t ppage;
         if (way < 0) {
             uint32_t old_st;
             uint64_t old_addr;
             int old_prog;
-            way = set_replace(v, meta, T.nways, T.offbits, T.idxbits, r.prog, &old_st, &old_addr, &old_prog);
+            way = set_replace(v, meta, tsa, T.nways, T.offbits, T.idxbits, r.prog, &old_st, &old_addr, &old_prog);
             if (old_st != ST_I) count(T.off_cnt, core, 2);
             count(T.off_cnt, core, 1);
             set_state(v, meta, way, ST_V);
             ppage = page_translate(r.prog, r.addr >> T.offbits);
-            if (ln == way) ppa[v.line0 + (uint64_t)way] = ppage;
+            if (ln == wl(v, way)) ppa[v.line0 + (uint64_t)way] = ppage;
             d += T.page_miss_delay;
+        } else if (wide(T.nways)) {
+            ppage = uni64(ppa[v.line0 + (uint64_t)way]);
         } else {
             ppage = rl64(mypp, way);
         }

@@ -37,7 +37,8 @@
 
 #define PU_QRING 128          // ring capacity (history tree holds <= 100 intervals)
 #define PU_QMAX 100           // QueueModelHistoryTree::_max_free_interval_size
-#define PU_MAX_WAYS 64
+#define PU_MAX_WAYS 64        // ways per set of the ahead-of-time kernels (one lane per way)
+#define PU_MAX_WAYS_WIDE 4096  // compiled configurations walk wider sets in 64-way chunks
 #define PU_MAX_NWORDS 1024    // sharer bitmap words -> up to 65536 LLC nodes (16-bit inline ids)
 
 // Network geometry helpers shared by host and engine.

@@ -102,7 +102,7 @@ int build_geo(const pu_sim_cfg* c, Geo* g, uint64_t pool_cap = 0) {
         const pu_cache_cfg& cc = y.cache[l];
         LevelGeo& L = g->lv[l];
         if (cc.share < 1 || cc.block_size < 1 || cc.num_ways < 1) return pu::set_error(PU_EINVAL, "bad cache geometry");
-        if (cc.num_ways > PU_MAX_WAYS) return pu::set_error(PU_ENOTSUP, "at most 64 ways per set");
+        if (cc.num_ways > PU_MAX_WAYS_WIDE) return pu::set_error(PU_ENOTSUP, "at most 4096 ways per set");
         L.nsets = cc.size / (cc.block_size * cc.num_ways);
         if (L.nsets < 1) return pu::set_error(PU_EINVAL, "cache has no sets");
         L.nways = cc.num_ways;
@@ -129,7 +129,7 @@ int build_geo(const pu_sim_cfg* c, Geo* g, uint64_t pool_cap = 0) {
     const pu_cache_cfg& dc = y.directory_cache;
     if (dc.size == 0) return pu::set_error(PU_EINVAL, "a directory is required (system.cpp:1052)");
     if (dc.num_ways < 1 || dc.block_size < 1) return pu::set_error(PU_EINVAL, "bad directory geometry");
-    if (dc.num_ways > PU_MAX_WAYS) return pu::set_error(PU_ENOTSUP, "at most 64 directory ways");
+    if (dc.num_ways > PU_MAX_WAYS_WIDE) return pu::set_error(PU_ENOTSUP, "at most 4096 directory ways");
     DirGeo& D = g->dir;
     D.nsets = dc.size / (dc.block_size * dc.num_ways);
     if (D.nsets < 1) return pu::set_error(PU_EINVAL, "directory has no sets");
@@ -184,7 +184,7 @@ int build_geo(const pu_sim_cfg* c, Geo* g, uint64_t pool_cap = 0) {
         const pu_cache_cfg& tc = y.tlb_cache;
         TlbGeo& T = g->tlb;
         if (tc.size == 0 || tc.num_ways < 1 || tc.block_size < 1) return pu::set_error(PU_EINVAL, "tlb_enable needs a TLB");
-        if (tc.num_ways > PU_MAX_WAYS) return pu::set_error(PU_ENOTSUP, "at most 64 TLB ways");
+        if (tc.num_ways > PU_MAX_WAYS_WIDE) return pu::set_error(PU_ENOTSUP, "at most 4096 TLB ways");
         if (y.page_size < 1) return pu::set_error(PU_EINVAL, "page_size must be >= 1");
         T.nsets = tc.size / (tc.block_size * tc.num_ways);
         if (T.nsets < 1) return pu::set_error(PU_EINVAL, "TLB has no sets");
@@ -318,6 +318,14 @@ struct pu_handle {
     } while (0)
 
 namespace {
+
+// the widest set of the configuration (cache levels, directory slices, TLBs)
+uint64_t max_ways(const Geo& g) {
+    uint64_t w = g.sys_type == 0 ? g.dir.nways : 0;
+    for (int l = 0; l < g.num_levels; l++) w = g.lv[l].nways > w ? g.lv[l].nways : w;
+    if (g.tlb_enable) w = g.tlb.nways > w ? g.tlb.nways : w;
+    return w;
+}
 
 int reset_state(pu_handle* h) {
     HIP_TRY(hipMemsetAsync(h->arena, 0, h->geo.replica_bytes * (size_t)h->R, h->stream), PU_EIO);
@@ -604,6 +612,9 @@ pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device) {
         return fail("hipMalloc of " + std::to_string(bytes) + " bytes for the replica arena failed");
     }
     if (pu::jit_load(geo, &h->jit, true) != 0) return fail(pu::g_err);
+    if (!h->jit.ok && max_ways(geo) > PU_MAX_WAYS)
+        return fail("sets of more than 64 ways run only in the compiled configuration (hipRTC, jit.cpp), which is "
+                    "unavailable (PRIMEUNCORE_JIT=0 or the compile failed)");
     h->sched.stat.assign((size_t)cfg->sys.num_cores, 0);
     h->rsched.resize((size_t)num_replicas);
     if (reset_state(h) != 0) {

@@ -36,3 +36,14 @@ def test_handle_reports_its_variant(jit, want, monkeypatch):
         assert uncore.lib().pu_compiled_config(um._handle()) == want
     finally:
         um.close()
+
+
+@pytest.mark.parametrize("name", ["dir_128way", "l1_tlb_128way", "bus_192way"])
+def test_wide_sets_need_the_compiled_configuration(name, monkeypatch):
+    """Sets of more than 64 ways are walked in 64-way chunks by the compiled
+    configuration only (their goldens run in test_gpu_golden); the
+    ahead-of-time kernels refuse them at pu_create instead of diverging."""
+    monkeypatch.setenv("PRIMEUNCORE_JIT", "0")
+    um = P.UncoreManager()
+    with pytest.raises(Exception, match="more than 64 ways"):
+        um.init(P.load_config(Case(name).xml_path), replicas=1)

@@ -103,6 +103,19 @@ def cases() -> dict:
     # Q7 with the config_prime default 30 MB / 24 W slice (20,480 sets)
     c["q7_default_dir"] = (_c1_shape(4, dir_size=31457280, dir_ways=24),
                            S(A.PU_STREAM_UNIFORM, 4, seed=9, num_quanta=3))
+    # sets wider than 64 ways (the engine walks them in 64-way chunks): a
+    # 128-way directory slice (8 sets), a 128-way L1 with a 128-entry fully
+    # associative TLB, a 192-way L1 on the snoopy bus
+    c["dir_128way"] = (_c1_shape(16, dir_size=65536, dir_ways=128),
+                       S(A.PU_STREAM_SHARED_UNIFORM, 16, seed=31, num_quanta=2))
+    wide = _c1_shape(16, tlb_enable=1, page_size=4096)
+    wide["system"]["cache"][0].update(size=16384, num_ways=128)
+    wide["system"]["tlb_cache"] = {"level": 0, "share": 1, "access_time": 1, "size": 128, "block_size": 1,
+                                   "num_ways": 128}
+    c["l1_tlb_128way"] = (wide, S(A.PU_STREAM_MULTIPROGRAM, 16, seed=32, num_quanta=2, num_progs=2))
+    bwide = _c1_shape(16, sys_type=1)
+    bwide["system"]["cache"][0].update(size=24576, num_ways=192)
+    c["bus_192way"] = (bwide, S(A.PU_STREAM_SHARED_UNIFORM, 16, seed=33, num_quanta=2))
     c["l2_shared_bus"] = (_l2_shared(64), S(A.PU_STREAM_MULTIPROGRAM, 64, seed=10, num_quanta=1, num_progs=2,
                                             max_requests=20000))
     c["three_level"] = (_three_level(64), S(A.PU_STREAM_SHARED_UNIFORM, 64, seed=12, num_quanta=1,
