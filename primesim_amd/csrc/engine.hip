@@ -252,7 +252,8 @@ __device__ __forceinline__ void err_or(uint64_t f) {
 enum ProfId {
     PF_LOOP, PF_REQ, PF_NET, PF_NSETUP, PF_NHOPS, PF_NTREE, PF_NWAIT, PF_NWB, PF_SETL0, PF_SETLN, PF_HOME_LD,
     PF_HOME, PF_DOWN, PF_WINDOWS, PF_TREEHOPS, PF_DEMAND, PF_T_LDS, PF_T_SEARCH, PF_T_DECIDE, PF_T_EDIT,
-    PF_T_STORE, PF_T_REFILL, PF_NPRE, PF_NPOST, PF_MG1RUN, PF_MG1LANES, PF_MG1HITS, PF_MAINTAIL, PF_COUNT
+    PF_T_STORE, PF_T_REFILL, PF_NPRE, PF_NPOST, PF_MG1RUN, PF_MG1LANES, PF_MG1HITS, PF_MAINTAIL,
+    PF_MG1PRESENT, PF_MG1STORED, PF_MG1BATCH, PF_COUNT
 };
 #ifdef PU_PROF
 static __shared__ unsigned long long lds_prof[PF_COUNT];
@@ -263,8 +264,10 @@ __device__ unsigned long long g_blk_t0[PU_PROF_BLOCKS], g_blk_t1[PU_PROF_BLOCKS]
 #define PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define PROF_ADD(id, t0) \
     do { if (lane_id() == 0) atomicAdd(&lds_prof[id], (unsigned long long)(__builtin_amdgcn_s_memtime() - (t0))); } while (0)
+// n is evaluated by the whole wave (it may be a ballot), then lane 0 adds it
 #define PROF_CNT(id, n) \
-    do { if (lane_id() == 0) atomicAdd(&lds_prof[id], (unsigned long long)(n)); } while (0)
+    do { const unsigned long long pf_n_ = (unsigned long long)(n); \
+         if (lane_id() == 0) atomicAdd(&lds_prof[id], pf_n_); } while (0)
 #else
 #define PROF_T(v)
 #define PROF_ADD(id, t0) do { } while (0)
@@ -908,6 +911,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         }
         PROF_CNT(PF_MG1LANES, (uint64_t)nh);
         PROF_CNT(PF_MG1HITS, (uint64_t)__builtin_popcountll(ballot(ln < nh && !need)));
+        PROF_CNT(PF_MG1PRESENT, (uint64_t)__builtin_popcountll(ballot(ln < nh && vcache != PU_MG1_CACHE_NONE)));
         uint64_t vfin = 0;              // t + d + p of hop h
         // Hop j arrives no earlier than LB_j = t + (j+1)*router + j*link_delay
         // (queue delays are >= 0).  A hop whose front free interval starts by
@@ -933,23 +937,39 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         // + link_delay), lane-parallel: assume every remaining hop takes M/G/1
         // (its delay is then known), get all arrival times with one wave
         // prefix scan, and find the first hop whose front interval starts by
-        // its arrival + p — the first tree hop.  Hops before it are final;
-        // the tree hop is done by the wave, and the scan restarts after it.
+        // its arrival + p — the first tree hop.  Hops before it are final; the
+        // tree hop is done by the wave.  Its delay d replaces the assumed
+        // M/G/1 wait, which moves every later arrival by the same d - wait:
+        // the latency mode (one wave alone, a dependent chain) carries that
+        // as one uniform shift `sh` (mod 2^64, like the sums); the throughput
+        // mode rescans after the tree hop (keeping the scan live across the
+        // tree operation costs registers there: -2.5% at 96 VGPRs, same-box).
+        uint64_t S = 0, A0 = 0, sh = 0;
+        const uint64_t t0 = t;
+        if constexpr (LH) {
+            const uint64_t e = ln < nh ? vd + c.link_delay + c.router : 0;
+            S = ballot(e >= (1ull << 26)) == 0 ? (uint64_t)scan_incl_u32((uint32_t)e) : scan_incl_u64(e);
+            A0 = t + c.router + (S - e);
+        }
         int js = 0;
         while (js < nh) {
             const bool live = ln >= js && ln < nh;
-            const uint64_t e = live ? vd + c.link_delay + c.router : 0;
-            // per-hop terms are small except past a saturated queue: a 32-bit
-            // scan then gives the same sums with a quarter of the VALU work
-            const uint64_t S = ballot(e >= (1ull << 26)) == 0 ? (uint64_t)scan_incl_u32((uint32_t)e)
-                                                                : scan_incl_u64(e);
-            const uint64_t A = t + c.router + (S - e);       // arrival of hop ln (after its router)
+            uint64_t A;
+            if constexpr (LH) {
+                A = A0 + sh;
+            } else {
+                const uint64_t e = live ? vd + c.link_delay + c.router : 0;
+                // per-hop terms are small except past a saturated queue: a 32-bit
+                // scan then gives the same sums with a quarter of the VALU work
+                S = ballot(e >= (1ull << 26)) == 0 ? (uint64_t)scan_incl_u32((uint32_t)e) : scan_incl_u64(e);
+                A = t + c.router + (S - e);                   // arrival of hop ln (after its router)
+            }
             const uint64_t cand = ballot(live && vfront <= A + (uint64_t)plen);
             const int jt = cand ? (int)__builtin_ctzll(cand) : nh;
             if (ln >= js && ln < jt) vfin = A + vd + (uint64_t)plen;
             mg1 += (uint64_t)(jt - js);
             if (jt == nh) {                                   // the rest of the window is M/G/1
-                t += rl64(S, nh - 1);
+                t = LH ? t0 + rl64(S, nh - 1) + sh : t + rl64(S, nh - 1);
                 break;
             }
             PROF_T(p_tree);
@@ -986,6 +1006,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                 issued++;
                 PROF_ADD(PF_T_REFILL, p_r);
             }
+            if constexpr (LH) sh += d - rl64(vd, jt);
             vhead = wl32(vhead, head, jt);
             vcnt = wl32(vcnt, cnt, jt);
             vf0 = wl64(vf0, f0n, jt);
@@ -1075,10 +1096,16 @@ __device__ void mg1_helper() {
             const QState st = hdr_state(a, b, v4u32{0u, 0u, 0u, 0u});   // M/G/1 needs a and b only
             const uint64_t w = mg1_wait(st);
             const uint64_t wmask = (1ull << PU_MG1_WAIT_BITS) - 1;
-            if (w < wmask && st.n < 4294967296.0)
+            const bool st_ok = w < wmask && st.n < 4294967296.0;
+            if (st_ok)
                 *(volatile AS3 uint64_t*)&lds_qhdr[(size_t)q * PU_LDS_SLOT + 3] =
                     w | ((uint64_t)((uint32_t)st.n & 0xFFFFFFu) << PU_MG1_WAIT_BITS);
+#ifdef PU_PROF
+            const uint64_t nst = __builtin_popcountll(ballot(st_ok));
+            if (ln == 0) atomicAdd(&lds_prof[PF_MG1STORED], (unsigned long long)nst);
+#endif
         }
+        PROF_CNT(PF_MG1BATCH, 1);
         tail += n;
     }
 }

@@ -19,8 +19,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF_LIB = os.environ.get("PROF_LIB") or os.path.join(ROOT, "primesim_amd", "libprimeuncore_prof.so")
 NAMES = ["LOOP", "REQ", "NET", "NSETUP", "NHOPS", "NTREE", "NWAIT", "NWB", "SETL0", "SETLN", "HOME_LD",
          "HOME", "DOWN", "windows", "tree_hops", "demand_hops", "T_LDS", "T_SEARCH", "T_DECIDE", "T_EDIT",
-         "T_STORE", "T_REFILL", "NPRE", "NPOST", "MG1RUN", "mg1_lanes", "mg1_cache_hits", "MAINTAIL"]
-COUNTS = {"windows", "tree_hops", "demand_hops", "mg1_lanes", "mg1_cache_hits"}
+         "T_STORE", "T_REFILL", "NPRE", "NPOST", "MG1RUN", "mg1_lanes", "mg1_cache_hits", "MAINTAIL",
+         "mg1_cache_present", "mg1_helper_stored", "mg1_helper_batches"]
+COUNTS = {"windows", "tree_hops", "demand_hops", "mg1_lanes", "mg1_cache_hits", "mg1_cache_present",
+          "mg1_helper_stored", "mg1_helper_batches"}
 
 
 def main() -> None:
