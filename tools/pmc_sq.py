@@ -69,7 +69,20 @@ def main() -> None:
         for name, per in vals.items():
             ids = sorted(per)[-steps:]
             out["per_launch"][name] = sum(per[k] for k in ids) / len(ids)
+    # accesses per launch of these runs (the bench line each pass printed)
+    acc = []
+    for i in range(len(PASSES)):
+        try:
+            with open(os.path.join(a.work, f"p{i}.log")) as f:
+                line = [ln for ln in f if ln.startswith("{")][-1]
+            b = json.loads(line)
+            acc.append(b["config"]["replicas_per_gpu"] * b["config"]["mean_requests_per_replica_per_step"])
+        except (OSError, IndexError, ValueError, KeyError):
+            pass
     pl = out["per_launch"]
+    if acc:
+        out["accesses_per_launch"] = sum(acc) / len(acc)
+        out["per_access"] = {k: v / out["accesses_per_launch"] for k, v in pl.items() if k.startswith("SQ_INSTS")}
     if pl.get("SQ_LDS_IDX_ACTIVE"):
         out["lds_bank_conflict_share"] = pl.get("SQ_LDS_BANK_CONFLICT", 0.0) / pl["SQ_LDS_IDX_ACTIVE"]
     if pl.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in pl:
