@@ -65,6 +65,10 @@ METRIC = "simulated memory accesses/sec (uncore) at 1024 cores; % HBM roofline"
 LIMITER = ("instruction issue and dependent-load latency (profiles/r3h_sq.json: 24% of wave cycles issuing, "
            "62% waiting on memory, 14% in issue stalls at 5 waves/SIMD), not HBM bandwidth")
 REQ_BYTES = 32          # sizeof(pu_req)
+VARIANTS = {0: "ahead-of-time kernels (runtime geometry) for every launch",
+            1: "ahead-of-time kernels for the replicas (throughput launches); the configuration compiled into "
+               "the kernel (hipRTC, jit.cpp) for one simulation alone (latency launches)",
+            2: "configuration compiled into the kernel (hipRTC, jit.cpp) for every launch"}
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 SEED_BASE = 4
 STAGE_GROUP = 256       # replicas whose requests the host generates per staging copy
@@ -497,7 +501,7 @@ class Device:
             self.um.allocCore(prog, th)
         self.stream = torch.cuda.Stream(self.dev)
         assert self.stream.cuda_stream != 0
-        self.compiled = P.uncore.lib().pu_compiled_config(self.um._handle()) == 1
+        self.compiled = P.uncore.lib().pu_compiled_config(self.um._handle())   # 0, 1 or 2 (primeuncore.h)
 
     def headline(self, args, rank: int, world: int):
         import primesim_amd as P
@@ -674,8 +678,7 @@ def main(argv=None) -> None:
                 "mg1_share_of_link_visits": H.delta["mg1_calls"] / max(1, H.delta["net_distance"]),
                 "error_flags": H.errf & ~A.PU_ERRF_NEG_DELAY,
                 "engine_build": P.uncore.library_source_hash(),
-                "engine_variant": ("configuration compiled into the kernel (hipRTC, jit.cpp)" if D.compiled else
-                                   "ahead-of-time kernels (runtime geometry)"),
+                "engine_variant": VARIANTS[D.compiled],
             },
             "per_simulation_accesses_per_s": value / tot_replicas,
             "single_instance": single,
@@ -688,7 +691,7 @@ def main(argv=None) -> None:
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": "pu_jit_uncore_s1_h0" if D.compiled else "uncore_kernel<1, true, false>",
+                "kernel": "pu_jit_uncore_s1_h0" if D.compiled == 2 else "uncore_kernel<1, true, false>",
                 "avg_launch_ms": avg_ms,
                 "alg_bytes_per_launch": bytes_per_launch,
                 "limiter": LIMITER,

@@ -241,8 +241,11 @@ long pu_config_geo_source(const pu_sim_cfg* cfg, char* buf, size_t cap);
  * kernels (the same engine source for a runtime geometry).  No reference
  * counterpart (the reference's System reads its XmlSys at run time).
  * pu_config_jit_warm compiles into the cache without a GPU (1: was cached,
- * 0: compiled, PU_E* on failure); pu_compiled_config tells whether handle h
- * runs the compiled configuration (1) or the ahead-of-time kernels (0). */
+ * 0: compiled, PU_E* on failure); pu_compiled_config tells what handle h
+ * runs: 0 the ahead-of-time kernels only; 1 the compiled configuration for
+ * latency launches (at most one replica per CU, headers in LDS) and the
+ * ahead-of-time kernels for throughput launches; 2 the compiled configuration
+ * for both (sets wider than 64 ways, or PRIMEUNCORE_JIT_THROUGHPUT=1). */
 int pu_config_jit_warm(const pu_sim_cfg* cfg);
 int pu_compiled_config(const pu_handle* h);
 /* Return all replicas to the just-initialised state (no reallocation). */

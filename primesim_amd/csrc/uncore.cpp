@@ -292,6 +292,7 @@ struct pu_handle {
     bool lds_headers_ok = false; // the replica's queue headers fit one CU's LDS
     bool lds_headers_short = false;   // latency mode for short host batches too
     pu::JitKernels jit;          // the engine compiled for this configuration (jit.cpp), if available
+    bool jit_throughput = false; // throughput launches (headers in HBM) also run the compiled configuration
     // ThreadSched (thread_sched.cpp): the shared one, and per-replica copies
     // made on first use of a per-replica call (pu_*_core_replica: the server's
     // sessions); the shared calls update both
@@ -406,7 +407,14 @@ int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const 
     const int lh = h->lds_headers_ok && nblocks <= h->cus && !short_launch ? 1 : 0;
     const uint32_t flags = (extra_flags & PU_KF_NOHALT) || !use_replay_mode ? extra_flags
                                                                           : (h->replay_flags | extra_flags);
-    int rc = h->jit.ok ? pu::jit_launch(h->jit, d_pos != nullptr, lh != 0, nblocks, s, h->d_geo, h->arena, replica0,
+    // latency launches run the compiled configuration; throughput launches run it
+    // only where the ahead-of-time kernels cannot (sets wider than 64 ways) or
+    // when asked (PRIMEUNCORE_JIT_THROUGHPUT=1): at C4, 96 VGPRs, the constant
+    // geometry spills 17 VGPRs to scratch (ahead-of-time: 3) and the headline ran
+    // 1.5% slower, while one simulation alone ran 23% faster (same-box A/B,
+    // profiles/r3i_ab_jit_*.txt)
+    const bool use_jit = h->jit.ok && (lh != 0 || h->jit_throughput);
+    int rc = use_jit ? pu::jit_launch(h->jit, d_pos != nullptr, lh != 0, nblocks, s, h->d_geo, h->arena, replica0,
                                         d_reqs, d_off, d_delay, d_pos, budget_ticks, flags)
                        : pu_engine_launch(h->d_geo, h->geo.num_levels, h->arena, replica0, nblocks, d_reqs, d_off,
                                           d_delay, d_pos, budget_ticks, flags, lh, s);
@@ -523,7 +531,7 @@ int pu_config_jit_warm(const pu_sim_cfg* cfg) {
     return pu::jit_warm(geo, nullptr);
 }
 
-int pu_compiled_config(const pu_handle* h) { return h && h->jit.ok ? 1 : 0; }
+int pu_compiled_config(const pu_handle* h) { return h && h->jit.ok ? (h->jit_throughput ? 2 : 1) : 0; }
 
 long pu_config_geo_source(const pu_sim_cfg* cfg, char* buf, size_t cap) {
     if (!cfg) return pu::set_error(PU_EINVAL, "bad arguments");
@@ -615,6 +623,10 @@ pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device) {
     if (!h->jit.ok && max_ways(geo) > PU_MAX_WAYS)
         return fail("sets of more than 64 ways run only in the compiled configuration (hipRTC, jit.cpp), which is "
                     "unavailable (PRIMEUNCORE_JIT=0 or the compile failed)");
+    if (h->jit.ok) {
+        const char* e = std::getenv("PRIMEUNCORE_JIT_THROUGHPUT");
+        h->jit_throughput = max_ways(geo) > PU_MAX_WAYS || (e && *e && std::atoi(e) != 0);
+    }
     h->sched.stat.assign((size_t)cfg->sys.num_cores, 0);
     h->rsched.resize((size_t)num_replicas);
     if (reset_state(h) != 0) {
@@ -655,7 +667,9 @@ int pu_resident_replicas(const pu_handle* h) {
     if (!h) return pu::set_error(PU_EINVAL, "null handle");
     int per_cu = 0, cus = 0;
     HIP_TRY(hipSetDevice(h->device), PU_ENODEV);
-    int rc = h->jit.ok ? pu::jit_occupancy(h->jit, &per_cu) : pu_engine_occupancy(h->geo.num_levels, &per_cu);
+    // the throughput kernel's occupancy (one wave per replica)
+    int rc = h->jit.ok && h->jit_throughput ? pu::jit_occupancy(h->jit, &per_cu)
+                                            : pu_engine_occupancy(h->geo.num_levels, &per_cu);
     if (rc) return pu::set_error(rc, "occupancy query failed");
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device), PU_EIO);
     return per_cu * cus;

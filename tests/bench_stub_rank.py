@@ -34,7 +34,7 @@ class StubDevice:
     def __init__(self, args, cfg, threads, rank, local):
         self.cfg, self.threads = cfg, threads
         self.R, self.um, self.dev, self.stream = REPLICAS, StubUM(), None, None
-        self.compiled = False
+        self.compiled = 0
 
     def headline(self, args, rank, world):
         import oracle as O
