@@ -20,7 +20,9 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "pu_jit_uncore_s1_h0"   # the timed launches of bench.py (compiled configuration; AOT: "uncore_kernel<1, true, false>")
+# the timed (throughput) launches of bench.py: the ahead-of-time kernel, or the
+# compiled configuration's under PRIMEUNCORE_JIT_THROUGHPUT=1
+KERNEL = "uncore_kernel<1, true, false>|pu_jit_uncore_s1_h0"
 PASSES = [
     ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"],
     ["SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_LDS", "SQ_INSTS_VALU",
@@ -37,7 +39,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", required=True)
     ap.add_argument("--work", default=os.path.join(ROOT, "gpurun_out", "pmc_sq"))
-    ap.add_argument("--kernel", default=KERNEL, help="kernel name substring to sum over")
+    ap.add_argument("--kernel", default=KERNEL, help="kernel name substrings to sum over, '|'-separated")
     ap.add_argument("bench_args", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     bargs = [x for x in a.bench_args if x != "--"]
@@ -61,7 +63,7 @@ def main() -> None:
         for fn in files:
             with open(fn) as fh:
                 for row in csv.DictReader(fh):
-                    if a.kernel not in row.get("Kernel_Name", ""):
+                    if not any(k in row.get("Kernel_Name", "") for k in a.kernel.split("|")):
                         continue
                     did = int(row["Dispatch_Id"])
                     vals.setdefault(row["Counter_Name"], {}).setdefault(did, 0.0)
