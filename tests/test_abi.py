@@ -60,6 +60,9 @@ def test_no_gpu_fails_loudly():
      "limited-pointer"),
     # the engine indexes a level's lines in 32 bits: 16 L1s of 2^36 B / 64 B = 2^34 lines
     (lambda s: s["system"]["cache"][0].update(size=1 << 36), "2^32 lines"),
+    # sets are walked in 64-way chunks up to 4,096 ways (compiled configuration)
+    (lambda s: s["system"]["cache"][0].update(size=8192 * 64, num_ways=8192), "4096 ways"),
+    (lambda s: s["system"]["directory_cache"].update(size=8192 * 64, num_ways=8192), "4096 directory ways"),
 ])
 def test_config_validation_before_device(mutate, msg):
     sim = CF.preset("C1")
@@ -73,7 +76,11 @@ def test_config_validation_before_device(mutate, msg):
 @pytest.mark.skipif(_gpu_present(), reason="checks the no-GPU path")
 @pytest.mark.parametrize("mutate", [lambda s: s["system"].update(tlb_enable=1),
                                     lambda s: s["system"].update(sys_type=1),
-                                    lambda s: s["system"].update(sys_type=1, tlb_enable=1)])
+                                    lambda s: s["system"].update(sys_type=1, tlb_enable=1),
+                                    # wide sets pass validation (the device decides the kernel variant)
+                                    lambda s: s["system"]["cache"][0].update(size=128 * 64, num_ways=128),
+                                    lambda s: s["system"]["directory_cache"].update(size=4096 * 64,
+                                                                                    num_ways=4096)])
 def test_bus_and_tlb_configs_are_accepted(mutate):
     """sys_type=1 (mesi_bus) and tlb_enable=1 pass validation: creation only stops at the missing device."""
     sim = CF.preset("C1")
