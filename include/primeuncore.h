@@ -242,10 +242,11 @@ long pu_config_geo_source(const pu_sim_cfg* cfg, char* buf, size_t cap);
  * counterpart (the reference's System reads its XmlSys at run time).
  * pu_config_jit_warm compiles into the cache without a GPU (1: was cached,
  * 0: compiled, PU_E* on failure); pu_compiled_config tells what handle h
- * runs: 0 the ahead-of-time kernels only; 1 the compiled configuration for
- * latency launches (at most one replica per CU, headers in LDS) and the
- * ahead-of-time kernels for throughput launches; 2 the compiled configuration
- * for both (sets wider than 64 ways, or PRIMEUNCORE_JIT_THROUGHPUT=1). */
+ * runs: 2 the compiled configuration for every launch (the default); 1 the
+ * compiled configuration for latency launches (at most one replica per CU,
+ * headers in LDS) and the ahead-of-time kernels for throughput launches
+ * (PRIMEUNCORE_JIT_THROUGHPUT=0; sets wider than 64 ways always take 2);
+ * 0 the ahead-of-time kernels only. */
 int pu_config_jit_warm(const pu_sim_cfg* cfg);
 int pu_compiled_config(const pu_handle* h);
 /* Return all replicas to the just-initialised state (no reallocation). */

@@ -57,6 +57,27 @@ namespace {
 #define PU_AOT_GEO(g) (g)
 #endif
 
+
+// Compiled configuration, throughput kernel: the replica-layout offsets reach
+// the code as opaque scalars (every other geometry value stays a constant).
+// Folded into the address arithmetic they cost the 96-VGPR kernel 17 VGPRs
+// spilled to scratch (opaque: 4; the latency kernel, with registers to spare,
+// keeps them folded): +4.6% on the C4 headline against the ahead-of-time
+// kernel, same box (profiles/r3o_ab_opq.txt).
+template <bool LH, int NL, class T>
+__device__ __forceinline__ T off_v(T c) {
+#ifdef PU_JIT_GEO
+    if constexpr (!LH && NL == 1) {   // (measured on the one-level engine; deeper hierarchies keep them folded)
+        // two 32-bit moves: a 64-bit SALU move takes only a 32-bit literal
+        uint32_t lo, hi;
+        asm("s_mov_b32 %0, %1" : "=s"(lo) : "s"((uint32_t)(uint64_t)c));
+        asm("s_mov_b32 %0, %1" : "=s"(hi) : "s"((uint32_t)((uint64_t)c >> 32)));
+        return (T)(((uint64_t)hi << 32) | lo);
+    }
+#endif
+    return c;
+}
+#define OFF(x) off_v<LH, NL>(x)
 constexpr uint32_t ST_I = 0, ST_S = 1, ST_E = 2, ST_M = 3, ST_V = 4, ST_B = 5;
 
 // Lane within the wavefront (latency-mode workgroups hold two waves).
@@ -828,14 +849,14 @@ static __shared__ uint32_t lds_dir_w[2][32];
 // branches.  The protocol code reaches it from four sites only.
 // Lane h prefetches hop h's link header and the two interval starts at its
 // ring head; only hops taking the tree branch fetch their full ring.
-template <bool LH>
+template <bool LH, int NL>
 __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char* base_in, int src, int dst, int len,
                                                  uint64_t timer, uint32_t& hq_head) {
     PROF_T(p_pre);
     NetCtx c;
     AS1 char* base = (AS1 char*)(char*)uni64((uint64_t)base_in);
-    c.qhdr = base + g->off_qhdr;
-    c.qring = base + g->off_qring;
+    c.qhdr = base + OFF(g->off_qhdr);
+    c.qring = base + OFF(g->off_qring);
     c.router = (uint32_t)g->router_delay;
     c.link_delay = (uint32_t)g->link_delay;
     c.inject = (uint32_t)g->inject_delay;
@@ -1137,8 +1158,8 @@ struct Engine {
     // ------------------------------------------------------------ network
     __device__ __forceinline__ NetCtx net_ctx() const {
         NetCtx c;
-        c.qhdr = (AS1 char*)base + g->off_qhdr;
-        c.qring = (AS1 char*)base + g->off_qring;
+        c.qhdr = (AS1 char*)base + OFF(g->off_qhdr);
+        c.qring = (AS1 char*)base + OFF(g->off_qring);
         c.router = (uint32_t)g->router_delay;
         c.link_delay = (uint32_t)g->link_delay;
         c.inject = (uint32_t)g->inject_delay;
@@ -1150,7 +1171,7 @@ struct Engine {
     }
     __device__ __forceinline__ uint64_t transmit(int src, int dst, int len, uint64_t timer) {
         PROF_T(p0);
-        uint64_t d = net_transmit<LH>(g, base, src, dst, len, timer, hq_head);
+        uint64_t d = net_transmit<LH, NL>(g, base, src, dst, len, timer, hq_head);
         PROF_ADD(PF_NET, p0);
         return d;
     }
@@ -1273,7 +1294,7 @@ struct Engine {
         // System::init_caches (system.cpp:172-207) creates the cache and its
         // ancestors on first touch; only the existence bit is observable.
         for (int k = l; k < NL; k++) {
-            if (ln == (cid & 63)) at<uint32_t>(g->lv[k].off_alive)[cid] = 1u;
+            if (ln == (cid & 63)) at<uint32_t>(OFF(g->lv[k].off_alive))[cid] = 1u;
             if (k + 1 < NL) cid = cid * g->lv[k].share / g->lv[k + 1].share;
         }
     }
@@ -1293,7 +1314,7 @@ struct Engine {
         const uint64_t bank = row & (uint64_t)(g->dram_banks - 1);
         const uint64_t page = (row >> g->dram_bank_shift) + 1;   // + 1: 0 means closed
         t = (int64_t)uni64((uint64_t)t);
-        DramBank* B = at<DramBank>(g->off_dram) + bank;
+        DramBank* B = at<DramBank>(OFF(g->off_dram)) + bank;
         const int64_t ready = (int64_t)uni64((uint64_t)B->ready);
         const uint64_t open = uni64(B->open);
         const int64_t start = ready > t ? ready : t;
@@ -1325,18 +1346,18 @@ struct Engine {
     template <int LV, bool INVAL>
     __device__ int down_impl(int cid, const Req& r) {
         const LevelGeo& L = g->lv[LV];
-        uint32_t alive_v = ln == (cid & 63) ? at<uint32_t>(L.off_alive)[cid] : 0u;
+        uint32_t alive_v = ln == (cid & 63) ? at<uint32_t>(OFF(L.off_alive))[cid] : 0u;
         SetView v;
-        set_load(v, at<LineMeta>(L.off_meta), at<int64_t>(L.off_ts), L.nsets, L.nways, L.offbits, L.idxbits,
+        set_load(v, at<LineMeta>(OFF(L.off_meta)), at<int64_t>(OFF(L.off_ts)), L.nsets, L.nways, L.offbits, L.idxbits,
                  (uint64_t)cid, r.addr);
         if (!rl32(alive_v, cid & 63)) return 0;   // cache never created: NULL in the reference
         stat_add(SN_LOCKDOWN, 1);
         int d = L.access_time;
-        int way = set_find(v, at<LineMeta>(L.off_meta), at<int64_t>(L.off_ts), L.nways, r.prog);
+        int way = set_find(v, at<LineMeta>(OFF(L.off_meta)), at<int64_t>(OFF(L.off_ts)), L.nways, r.prog);
         if (way >= 0) {
             uint32_t st = rl32(v.mst, wl(v, way));
             if (INVAL || st == ST_M || st == ST_E) {
-                set_state(v, at<LineMeta>(L.off_meta), way, INVAL ? ST_I : ST_S);
+                set_state(v, at<LineMeta>(OFF(L.off_meta)), way, INVAL ? ST_I : ST_S);
                 d += children<LV, INVAL>(cid, r);
             }
         }
@@ -1387,7 +1408,7 @@ struct Engine {
                        ((s & 0xFFF000000000ull) << 12);
     }
     __device__ __forceinline__ uint64_t* pool_of(uint64_t idx) const {
-        return at<uint64_t>(g->dir.off_pool) + idx * (uint64_t)g->dir.nwords;
+        return at<uint64_t>(OFF(g->dir.off_pool)) + idx * (uint64_t)g->dir.nwords;
     }
     // bitmap words base .. base+63 of pool entry idx, lane k holding word base + k
     __device__ __forceinline__ uint64_t pool_word(uint64_t idx, int base = 0) const {
@@ -1396,7 +1417,7 @@ struct Engine {
     __device__ __forceinline__ void pool_release(uint32_t nsh, uint64_t sh) {
         if (nsh != PU_SH_POOL) return;
         const int32_t pt = (int32_t)uni32((uint32_t)lds_eng.pool_top);
-        if (ln == 0) at<int32_t>(g->dir.off_pool_free)[pt] = (int32_t)sh;
+        if (ln == 0) at<int32_t>(OFF(g->dir.off_pool_free))[pt] = (int32_t)sh;
         lds_eng.pool_top = pt + 1;
     }
     __device__ __forceinline__ bool pool_alloc(uint64_t* idx) {
@@ -1407,7 +1428,7 @@ struct Engine {
             return false;
         }
         lds_eng.pool_top = pt - 1;
-        uint32_t v = ln == 0 ? (uint32_t)at<int32_t>(g->dir.off_pool_free)[pt - 1] : 0u;
+        uint32_t v = ln == 0 ? (uint32_t)at<int32_t>(OFF(g->dir.off_pool_free))[pt - 1] : 0u;
         *idx = rl32(v, 0);
         return true;
     }
@@ -1550,7 +1571,7 @@ struct Engine {
         const uint64_t set = set_index(addr, D.offbits, D.nsets);
         const uint64_t line0 = (uint64_t)(((uint32_t)home * (uint32_t)D.csets + (uint32_t)(set >> D.cset_shift)) * (uint32_t)D.nways);
         if ((uint64_t)ln < D.nways) {
-            const AS1 char* lp = (const AS1 char*)(const char*)(at<DirLine>(D.off_line) + line0 + (uint64_t)ln);
+            const AS1 char* lp = (const AS1 char*)(const char*)(at<DirLine>(OFF(D.off_line)) + line0 + (uint64_t)ln);
             lds_dma<true>(lp, lds_addr(&lds_dir_a[0]));
             lds_dma<false>(lp + 16, lds_addr(&lds_dir_w[0][0]));
             lds_dma<false>(lp + 20, lds_addr(&lds_dir_w[1][0]));
@@ -1570,8 +1591,8 @@ struct Engine {
         const bool shared = g->shared_llc != 0;
         constexpr int last = NL - 1;
         const int blk = (int)g->lv[last].block;
-        DirLine* lines = at<DirLine>(D.off_line);
-        if (ln == (home & 63)) at<uint32_t>(D.off_alive)[home] = 1u;   // home_stat[home] = 1
+        DirLine* lines = at<DirLine>(OFF(D.off_line));
+        if (ln == (home & 63)) at<uint32_t>(OFF(D.off_alive))[home] = 1u;   // home_stat[home] = 1
         const uint64_t set = set_index(r.addr, D.offbits, D.nsets);
         const uint64_t tag = r.addr >> (D.offbits + D.idxbits);
         const uint64_t line0 = (uint64_t)(((uint32_t)home * (uint32_t)D.csets + (uint32_t)(set >> D.cset_shift)) * (uint32_t)D.nways);
@@ -1604,7 +1625,7 @@ struct Engine {
         // program ids: the 10-bit field decides unless either side is escaped;
         // the side array is read only then (ids >= 1023 or negative)
         const uint32_t want10 = prog10(r.prog), m_p10 = (uint32_t)(m.w >> 54);
-        int32_t* side = at<int32_t>(D.off_prog);
+        int32_t* side = at<int32_t>(OFF(D.off_prog));
         int32_t m_prog = (int32_t)m_p10;
         if (want10 == PU_DIR_PROG_ESC || ballot(mine && m_p10 == PU_DIR_PROG_ESC)) {
             if (mine && m_p10 == PU_DIR_PROG_ESC) m_prog = side[line0 + (uint64_t)ln];
@@ -1636,7 +1657,7 @@ struct Engine {
             }
         }
         PROF_ADD(PF_HOME_LD, p_ld);
-        count(D.off_cnt, home, 0);
+        count(OFF(D.off_cnt), home, 0);
         int delay = D.access_time;
         uint32_t st, nsh;
         uint64_t sh;
@@ -1692,7 +1713,7 @@ struct Engine {
             }
             dir_sharers(ww, nsh, sh);
             if (old_st != ST_I) {
-                count(D.off_cnt, home, 2);
+                count(OFF(D.off_cnt), home, 2);
                 pr = Req{old_addr, old_prog, PU_RD};
                 if (old_st == ST_M || old_st == ST_E) {
                     pmode = PR_ONE;
@@ -1706,7 +1727,7 @@ struct Engine {
                 }
             }
             st = r.type == PU_WR ? ST_M : ST_E;
-            count(D.off_cnt, home, 1);
+            count(OFF(D.off_cnt), home, 1);
             release_set = true;
             miss_fill = true;
         } else if (way < 0) {
@@ -1796,8 +1817,8 @@ struct Engine {
     __device__ uint32_t mesi(int cid, const Req& r, int64_t timer) {
         const LevelGeo& L = g->lv[LV];
         constexpr bool kLast = LV == NL - 1;
-        LineMeta* meta = at<LineMeta>(L.off_meta);
-        int64_t* tsa = at<int64_t>(L.off_ts);
+        LineMeta* meta = at<LineMeta>(OFF(L.off_meta));
+        int64_t* tsa = at<int64_t>(OFF(L.off_ts));
         SetView v;
         PROF_T(p_set);
         set_load(v, meta, tsa, L.nsets, L.nways, L.offbits, L.idxbits, (uint64_t)cid, r.addr);
@@ -1811,7 +1832,7 @@ struct Engine {
             stat_add(SN_BUSCONT, (uint64_t)(int64_t)db);
             dly += db;
         }
-        if (!hit) count(L.off_cnt, cid, 0);
+        if (!hit) count(OFF(L.off_cnt), cid, 0);
         dly += L.access_time;
         int way = set_find(v, meta, tsa, L.nways, r.prog);
         PROF_ADD(LV == 0 ? PF_SETL0 : PF_SETLN, p_set);
@@ -1852,11 +1873,11 @@ struct Engine {
             int old_prog;
             way = set_replace(v, meta, tsa, L.nways, L.offbits, L.idxbits, r.prog, &old_st, &old_addr, &old_prog);
             if (old_st != ST_I) {
-                count(L.off_cnt, cid, 2);
+                count(OFF(L.off_cnt), cid, 2);
                 Req o{old_addr, old_prog, PU_RD};
                 dly += children<LV, true>(cid, o);
                 if (old_st == ST_M || old_st == ST_E) {
-                    count(L.off_cnt, cid, 3);
+                    count(OFF(L.off_cnt), cid, 3);
                     if constexpr (kLast) {
                         tx_wb = true;
                         wb_home = home_of(old_addr);
@@ -1908,7 +1929,7 @@ struct Engine {
             }
             set_state(v, meta, way, is_miss ? ret : ST_M);
         }
-        if (is_miss) count(L.off_cnt, cid, 1);
+        if (is_miss) count(OFF(L.off_cnt), cid, 1);
         return ret;
     }
 
@@ -1931,7 +1952,7 @@ struct Engine {
     __device__ bool snoop(int cid, const Req& r, int mode) {
         constexpr int last = NL - 1;
         const LevelGeo& L = g->lv[last];
-        LineMeta* meta = at<LineMeta>(L.off_meta);
+        LineMeta* meta = at<LineMeta>(OFF(L.off_meta));
         const uint64_t set = set_index(r.addr, L.offbits, L.nsets);
         const uint64_t tag = r.addr >> (L.offbits + L.idxbits);
         bool any = false;
@@ -1970,8 +1991,8 @@ struct Engine {
     __device__ uint32_t mesi_bus(int cid, const Req& r, int64_t timer) {
         const LevelGeo& L = g->lv[LV];
         constexpr bool kLast = LV == NL - 1;
-        LineMeta* meta = at<LineMeta>(L.off_meta);
-        int64_t* tsa = at<int64_t>(L.off_ts);
+        LineMeta* meta = at<LineMeta>(OFF(L.off_meta));
+        int64_t* tsa = at<int64_t>(OFF(L.off_ts));
         SetView v;
         set_load(v, meta, tsa, L.nsets, L.nways, L.offbits, L.idxbits, (uint64_t)cid, r.addr);
         mark_alive(LV, cid);
@@ -1985,7 +2006,7 @@ struct Engine {
             dly += db;
         }
         dly += L.access_time;
-        if (!hit) count(L.off_cnt, cid, 0);
+        if (!hit) count(OFF(L.off_cnt), cid, 0);
         int way = set_find(v, meta, tsa, L.nways, r.prog);
         bool is_miss = false, call_parent = false;
         int snoop_mode = -1;
@@ -2039,7 +2060,7 @@ struct Engine {
             }
         }
         if (is_miss) {
-            count(L.off_cnt, cid, 1);
+            count(OFF(L.off_cnt), cid, 1);
             return ret;
         }
         children<LV, true>(cid, r);                          // write hit: inval_children, discarded
@@ -2054,7 +2075,7 @@ struct Engine {
     // first empty slot.
     __device__ uint64_t page_translate(int prog, uint64_t vpage) {
         const TlbGeo& T = g->tlb;
-        PageEnt* tab = at<PageEnt>(T.off_pages);
+        PageEnt* tab = at<PageEnt>(OFF(T.off_pages));
         const uint64_t mask = T.pages_cap - 1;
         uint64_t x = vpage * 0x9E3779B97F4A7C15ull ^ ((uint64_t)(uint32_t)prog * 0xC2B2AE3D27D4EB4Full);
         x ^= x >> 31;
@@ -2090,13 +2111,13 @@ struct Engine {
     // request's address becomes physical (ppage << log2(page) | offset).
     __device__ int tlb_translate(int core, Req& r, int64_t timer) {
         const TlbGeo& T = g->tlb;
-        LineMeta* meta = at<LineMeta>(T.off_meta);
-        int64_t* tsa = at<int64_t>(T.off_ts);
-        uint64_t* ppa = at<uint64_t>(T.off_ppage);
+        LineMeta* meta = at<LineMeta>(OFF(T.off_meta));
+        int64_t* tsa = at<int64_t>(OFF(T.off_ts));
+        uint64_t* ppa = at<uint64_t>(OFF(T.off_ppage));
         SetView v;
         set_load(v, meta, tsa, T.nsets, T.nways, T.offbits, T.idxbits, (uint64_t)core, r.addr);
         const uint64_t mypp = !wide(T.nways) && (uint64_t)ln < T.nways ? ppa[v.line0 + (uint64_t)ln] : 0ull;
-        count(T.off_cnt, core, 0);
+        count(OFF(T.off_cnt), core, 0);
         int d = T.access_time;
         int way = set_find(v, meta, tsa, T.nways, r.prog);
         uint64_t ppage;
@@ -2105,8 +2126,8 @@ struct Engine {
             uint64_t old_addr;
             int old_prog;
             way = set_replace(v, meta, tsa, T.nways, T.offbits, T.idxbits, r.prog, &old_st, &old_addr, &old_prog);
-            if (old_st != ST_I) count(T.off_cnt, core, 2);
-            count(T.off_cnt, core, 1);
+            if (old_st != ST_I) count(OFF(T.off_cnt), core, 2);
+            count(OFF(T.off_cnt), core, 1);
             set_state(v, meta, way, ST_V);
             ppage = page_translate(r.prog, r.addr >> T.offbits);
             if (ln == wl(v, way)) ppa[v.line0 + (uint64_t)way] = ppage;
@@ -2142,7 +2163,7 @@ struct Engine {
 
     __device__ void flush_stats() {
         if (ln != 0) return;
-        EngineStats* S = at<EngineStats>(g->off_stats);
+        EngineStats* S = at<EngineStats>(OFF(g->off_stats));
         // Network::transmit's per-packet router term (hops+1)*router, inject
         // term and link remainder total - router - (plen-1) - inject, summed
         // (mod 2^64, as the per-packet sums are)
@@ -2213,7 +2234,7 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
         // Latency mode: a two-wave workgroup.  Both waves copy the replica's
         // queue headers into the LDS image (pieces a, b, c; d = no cached
         // wait); wave 0 simulates, wave 1 is the M/G/1 helper (mg1_helper).
-        const AS1 v4u32* gh = (const AS1 v4u32*)(AS1 char*)(e.base + e.g->off_qhdr);
+        const AS1 v4u32* gh = (const AS1 v4u32*)(AS1 char*)(e.base + OFF(e.g->off_qhdr));
         const uint32_t nq4 = (uint32_t)e.g->nqueues * PU_LDS_SLOT;
         for (uint32_t k = threadIdx.x; k < nq4; k += 128)
             lds_qhdr[k] = (k & 3u) < 3u ? gh[(k >> 2) * PU_HDR_PIECES + (k & 3u)] : v4u32{~0u, ~0u, 0u, 0u};
@@ -2225,7 +2246,7 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
             __syncthreads();                              // [1] stats_init's
             mg1_helper();
             __syncthreads();                              // [2] the main wave left its loop
-            AS1 v4u32* gho = (AS1 v4u32*)(AS1 char*)(e.base + e.g->off_qhdr);
+            AS1 v4u32* gho = (AS1 v4u32*)(AS1 char*)(e.base + OFF(e.g->off_qhdr));
             for (uint32_t k = threadIdx.x; k < nq4; k += 128)
                 if ((k & 3u) < 3u) gho[(k >> 2) * PU_HDR_PIECES + (k & 3u)] = lds_qhdr[k];
             __syncthreads();                              // [3] before the stats flush
@@ -2243,7 +2264,7 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
     // The message loop's own state lives in LDS (lane 0 writes, every lane reads
     // it back wave-uniform): nothing of it stays in registers across the
     // inlined access(), whose register budget is tight (4 waves/SIMD).
-    RunState* rs = e.template at<RunState>(e.g->off_run);
+    RunState* rs = e.template at<RunState>(OFF(e.g->off_run));
     if (e.ln == 0) {
         const int32_t h0 = rs->halted;
         lds_ctl.D = rs->batch_delay;
@@ -2278,7 +2299,7 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
             lds_ctl.D = 0;
             lds_ctl.skip = (fl & PU_KF_MSGHALT) ? (int32_t)((lds_ctl.dead_tags >> (q.tag & 63)) & 1) : 0;
             if ((fl & PU_KF_CLOSED) && core_ok)
-                lds_ctl.msg_shift = e.template at<int64_t>(e.g->off_core_shift)[q.core];
+                lds_ctl.msg_shift = e.template at<int64_t>(OFF(e.g->off_core_shift))[q.core];
         }
         __builtin_amdgcn_wave_barrier();
         if (uni32((uint32_t)lds_ctl.skip)) {     // PU_KF_MSGHALT: this message's receive thread has exited
@@ -2296,9 +2317,9 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
             lds_ctl.done++;
             delays[i] = d;
             if (core_ok) {
-                e.template at<int64_t>(e.g->off_completion)[q.core] = t + d;
+                e.template at<int64_t>(OFF(e.g->off_completion))[q.core] = t + d;
                 if (lds_ctl.flags & PU_KF_CLOSED)
-                    e.template at<int64_t>(e.g->off_core_shift)[q.core] = lds_ctl.msg_shift + D;
+                    e.template at<int64_t>(OFF(e.g->off_core_shift))[q.core] = lds_ctl.msg_shift + D;
             }
             if (D < 0) {                         // prime.cpp:130-134
                 err_or(PU_ERRF_NEG_DELAY);
@@ -2321,7 +2342,7 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
     if constexpr (LH) {                                   // ... and the headers back
         if (e.ln == 0) *(volatile AS3 uint32_t*)&lds_main_done = 1u;
         __syncthreads();                                  // [2]
-        AS1 v4u32* gh = (AS1 v4u32*)(AS1 char*)(e.base + e.g->off_qhdr);
+        AS1 v4u32* gh = (AS1 v4u32*)(AS1 char*)(e.base + OFF(e.g->off_qhdr));
         const uint32_t nq4 = (uint32_t)e.g->nqueues * PU_LDS_SLOT;
         for (uint32_t k = threadIdx.x; k < nq4; k += 128)
             if ((k & 3u) < 3u) gh[(k >> 2) * PU_HDR_PIECES + (k & 3u)] = lds_qhdr[k];

@@ -293,6 +293,7 @@ struct pu_handle {
     bool lds_headers_short = false;   // latency mode for short host batches too
     pu::JitKernels jit;          // the engine compiled for this configuration (jit.cpp), if available
     bool jit_throughput = false; // throughput launches (headers in HBM) also run the compiled configuration
+                                 // (the default; PRIMEUNCORE_JIT_THROUGHPUT=0 keeps them ahead-of-time)
     // ThreadSched (thread_sched.cpp): the shared one, and per-replica copies
     // made on first use of a per-replica call (pu_*_core_replica: the server's
     // sessions); the shared calls update both
@@ -407,12 +408,10 @@ int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const 
     const int lh = h->lds_headers_ok && nblocks <= h->cus && !short_launch ? 1 : 0;
     const uint32_t flags = (extra_flags & PU_KF_NOHALT) || !use_replay_mode ? extra_flags
                                                                           : (h->replay_flags | extra_flags);
-    // latency launches run the compiled configuration; throughput launches run it
-    // only where the ahead-of-time kernels cannot (sets wider than 64 ways) or
-    // when asked (PRIMEUNCORE_JIT_THROUGHPUT=1): at C4, 96 VGPRs, the constant
-    // geometry spills 17 VGPRs to scratch (ahead-of-time: 3) and the headline ran
-    // 1.5% slower, while one simulation alone ran 23% faster (same-box A/B,
-    // profiles/r3i_ab_jit_*.txt)
+    // latency launches run the compiled configuration (one simulation alone +23%
+    // over the ahead-of-time kernel, profiles/r3i_ab_jit_single.txt); throughput
+    // launches too (+4.6% at C4 with the replica-layout offsets kept opaque,
+    // profiles/r3o_ab_opq.txt) unless PRIMEUNCORE_JIT_THROUGHPUT=0
     const bool use_jit = h->jit.ok && (lh != 0 || h->jit_throughput);
     int rc = use_jit ? pu::jit_launch(h->jit, d_pos != nullptr, lh != 0, nblocks, s, h->d_geo, h->arena, replica0,
                                         d_reqs, d_off, d_delay, d_pos, budget_ticks, flags)
@@ -625,7 +624,7 @@ pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device) {
                     "unavailable (PRIMEUNCORE_JIT=0 or the compile failed)");
     if (h->jit.ok) {
         const char* e = std::getenv("PRIMEUNCORE_JIT_THROUGHPUT");
-        h->jit_throughput = max_ways(geo) > PU_MAX_WAYS || (e && *e && std::atoi(e) != 0);
+        h->jit_throughput = max_ways(geo) > PU_MAX_WAYS || !(e && *e && std::atoi(e) == 0);
     }
     h->sched.stat.assign((size_t)cfg->sys.num_cores, 0);
     h->rsched.resize((size_t)num_replicas);

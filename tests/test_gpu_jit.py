@@ -3,13 +3,13 @@ into the kernel (jit.cpp, hipRTC; the default) and the ahead-of-time kernels
 (PRIMEUNCORE_JIT=0) that read the geometry at run time.
 
 By default (pu_create; the cache is warmed by __graft_entry__.build()) a
-handle runs the compiled configuration for its latency launches (at most one
-replica per CU, headers in LDS: the long golden batches) and the ahead-of-time
-kernels for throughput launches (short batches, many replicas).  Here a spread
-of goldens (one and three levels, bus system, TLB, limited pointer, 3-D mesh,
-closed loop, a full-size digest) also runs with the ahead-of-time kernels only
-(PRIMEUNCORE_JIT=0) and with the compiled configuration for every launch
-(PRIMEUNCORE_JIT_THROUGHPUT=1), and every handle reports its variant.
+handle runs the compiled configuration for every launch: latency launches (at
+most one replica per CU, headers in LDS: the long golden batches) and
+throughput launches (short batches, many replicas).  Here a spread of goldens
+(one and three levels, bus system, TLB, limited pointer, 3-D mesh, closed
+loop, a full-size digest) also runs with the ahead-of-time kernels only
+(PRIMEUNCORE_JIT=0) and with the ahead-of-time kernels for the throughput
+launches (PRIMEUNCORE_JIT_THROUGHPUT=0), and every handle reports its variant.
 """
 import pytest
 
@@ -25,10 +25,10 @@ CASES = ["c1_hot", "c3_multiprog", "three_level", "bus_c2", "tlb_c3", "limited_p
 
 
 @pytest.mark.parametrize("name", ["c1_hot", "c3_multiprog", "bus_c2", "tlb_c3", "c4_closed", "big_c4_quantum"])
-def test_compiled_configuration_on_throughput_launches_matches_reference(name, monkeypatch):
-    """PRIMEUNCORE_JIT_THROUGHPUT=1: the compiled configuration also runs the
-    throughput launches (the default runs it for latency launches only)."""
-    monkeypatch.setenv("PRIMEUNCORE_JIT_THROUGHPUT", "1")
+def test_ahead_of_time_throughput_launches_match_reference(name, monkeypatch):
+    """PRIMEUNCORE_JIT_THROUGHPUT=0: throughput launches on the ahead-of-time
+    kernels, latency launches on the compiled configuration."""
+    monkeypatch.setenv("PRIMEUNCORE_JIT_THROUGHPUT", "0")
     test_engine_reproduces_reference(name)
 
 
@@ -38,7 +38,7 @@ def test_ahead_of_time_kernels_match_reference(name, monkeypatch):
     test_engine_reproduces_reference(name)
 
 
-@pytest.mark.parametrize("jit,thr,want", [("1", "0", 1), ("1", "1", 2), ("0", "0", 0)])
+@pytest.mark.parametrize("jit,thr,want", [("1", "0", 1), ("1", "1", 2), ("1", "", 2), ("0", "0", 0)])
 def test_handle_reports_its_variant(jit, thr, want, monkeypatch):
     monkeypatch.setenv("PRIMEUNCORE_JIT", jit)
     monkeypatch.setenv("PRIMEUNCORE_JIT_THROUGHPUT", thr)
