@@ -102,9 +102,13 @@ void write_file_atomic(const std::string& path, const std::vector<char>& data) {
 }
 
 std::vector<std::string> options(int waves_1level) {
+    // max-occupancy: at C4 the throughput kernel spills 2 VGPRs instead of 4
+    // and ran ahead of max-ILP in each of three interleaved rounds (233.0 /
+    // 230.0 / 232.7 vs 215.9 / 226.9 / 231.4 M/s), one simulation alone level
+    // (profiles/r3q_ab_occ*.txt); the ahead-of-time kernels keep max-ILP
     std::vector<std::string> o = {"--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-fwrapv",
-                                  "-mllvm", "-amdgpu-sched-strategy=max-ilp", "-DPU_JIT_GEO=\"pu_jit_geo.h\"",
-                                  "-Wno-c99-designator"};
+                                  "-mllvm", "-amdgpu-sched-strategy=max-occupancy",
+                                  "-DPU_JIT_GEO=\"pu_jit_geo.h\"", "-Wno-c99-designator"};
     if (waves_1level > 0) o.push_back("-DPU_WAVES_1LEVEL=" + std::to_string(waves_1level));
     return o;
 }
