@@ -1,6 +1,6 @@
 # Final measurements of the shipped build: GPU suite, smoke, PMC fabric traffic (same build), the driver's
 # bench config carrying that traffic, rocprofv3 kernel stats of the same command.  tools/r3_final.sh TAG
-T=${1:-r3j}
+T=${1:-r3r}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/${T}_gpu_tests.log 2>&1 || exit 1
