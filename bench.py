@@ -13,16 +13,23 @@ of --chunk (40,960) requests of its own stream untimed (a C4 quantum is
 core is active; cold caches and empty link histories are warmed).  The next
 --steps x --chunk requests are then made resident in HBM and each timed "step"
 is one engine launch (prime.cpp's message loop over System::access) in which
-every replica continues its own stream for a --slice-ms wall-time slice,
-stopping only between requests (pu_run_device_sliced): replicas differ
-several-fold in cost per request, and the slice keeps every wave simulating.
-A replica is one complete, independent 1024-core uncore (its own seed), one
-per wavefront.  `value` = all requests processed by all ranks / max-over-ranks
-wall time of the K timed steps.  Replay is open loop (recorded timers).
+every wavefront continues its replica's stream for a --slice-ms wall-time
+slice, stopping only between requests: replicas differ several-fold in cost
+per request, and the slice keeps every wave simulating.  A replica is one
+complete, independent 1024-core uncore (its own seed), simulated by one
+wavefront at a time.  The GPU holds one wavefront per resident slot and
+--spare-replicas more replicas (all warmed alike): a wavefront whose replica
+stops by prime.cpp's rule (open-loop overload) or finishes its window takes
+the next unstarted replica within the slice (the replica pool,
+pu_run_device_pool), so no slot idles.  `value` = all requests processed by
+all ranks / max-over-ranks wall time of the K timed steps.  Replay is open
+loop (recorded timers).
 
 At N=1 (rank 0) the same line also carries:
-  * per_simulation_accesses_per_s — value / replicas: the rate of ONE of the
+  * per_simulation_accesses_per_s — value / wavefronts: the rate of ONE of the
     concurrent simulations;
+  * replica_parity — the delays of 16 replicas spread over 0..R-1 (warmup and
+    timed window) against the reference's, replayed by the ensemble processes;
   * single_instance — ONE simulation alone on the GPU (a 1-replica engine on
     replica 0's stream, same warmup, then --single-requests in one launch);
   * closed_loop — the same workload replayed closed-loop (timer_i += the core's
@@ -170,50 +177,82 @@ def cpu_baseline(cfg_xml: str, cfg, reqs: np.ndarray, threads, fill: int, budget
 
 
 # ---------------------------------------------------------------- CPU ensemble
-def _ensemble_worker(conn, cfg_xml: str, seed: int, fill: int, n_timed: int, budget_s: float) -> None:
-    """One replica of the ensemble: fill untimed, wait for "go", run for budget_s."""
+def _ensemble_worker(conn, cfg_xml: str, fill: int, n_timed: int, budget_s: float) -> None:
+    """One replica of the ensemble: wait for its replica index (the parent
+    knows the replica count only once it has the GPU), fill untimed, wait for
+    "go", run for budget_s; send back every delay it produced (parity)."""
     try:
+        msg = conn.recv()
+        if msg[0] != "replica":
+            return
+        rep = int(msg[1])
         import primesim_amd as P
+        from primesim_amd.dist import replica_seed
         cfg = P.load_config(cfg_xml)
-        reqs = P.generate_stream(stream_spec(seed, fill + n_timed))
-        threads = P.stream_threads(stream_spec(seed))
+        reqs = P.generate_stream(stream_spec(replica_seed(SEED_BASE, 0, rep), fill + n_timed))
+        threads = P.stream_threads(stream_spec(SEED_BASE))
         kind, eng = reference_engine(cfg_xml, cfg)
         for prog, th in threads:
             eng.alloc_core(prog, th)
+        delays = []
         for a in range(0, fill, 16384):
-            eng.run(reqs[a:min(fill, a + 16384)])
+            d, _ = eng.run(reqs[a:min(fill, a + 16384)])
+            delays.append(d)
         conn.send(("ready", kind))
         conn.recv()                                   # go
         done, sim, t0 = fill, 0, time.perf_counter()
         while done < len(reqs) and time.perf_counter() - t0 < budget_s:
             d, rc = eng.run(reqs[done:done + 2048])
+            delays.append(d)
             done += len(d)
             sim += simulated(len(d), rc)
             if rc != 0:                               # halted: the rest would only be skipped
                 break
-        conn.send(("done", sim, time.perf_counter() - t0))
+        el = time.perf_counter() - t0
+        conn.send(("done", sim, el, rep, np.concatenate(delays).astype(np.int32).tobytes()))
     except Exception as e:  # noqa: BLE001 — reported to the parent
         conn.send(("error", repr(e)))
     finally:
         conn.close()
 
 
+def parity_replicas(R: int, workers: int) -> list:
+    """Replicas the ensemble replays: spread over 0..R-1, the last one R-1."""
+    if workers <= 1 or R <= 1:
+        return [0][:workers]
+    step = max(1, R // workers)
+    reps = [min(w * step, R - 1) for w in range(workers - 1)] + [R - 1]
+    return sorted(set(reps))
+
+
 class Ensemble:
     """The reference uncore on every host core of this job's share, one replica
-    per process, forked before the parent touches the GPU."""
+    per process, forked before the parent touches the GPU.  Each process is
+    told its replica once the parent knows the replica count (assign), fills
+    while the GPU warms up, and returns its delays: the parity check of those
+    replicas against the GPU's."""
 
     def __init__(self, cfg_xml: str, workers: int, fill: int, n_timed: int, budget_s: float):
         ctx = mp.get_context("fork")
         self.workers, self.budget = workers, budget_s
         self.fill = fill
         self.pipes, self.procs = [], []
+        self.replicas: list = []
         for w in range(workers):
             a, b = ctx.Pipe()
-            p = ctx.Process(target=_ensemble_worker, args=(b, cfg_xml, SEED_BASE + w, fill, n_timed, budget_s),
-                            daemon=True)
+            p = ctx.Process(target=_ensemble_worker, args=(b, cfg_xml, fill, n_timed, budget_s), daemon=True)
             p.start()
             self.pipes.append(a)
             self.procs.append(p)
+
+    def assign(self, R: int) -> list:
+        self.replicas = parity_replicas(R, self.workers)
+        for k, c in enumerate(self.pipes):
+            c.send(("replica", self.replicas[k]) if k < len(self.replicas) else ("stop",))
+        self.pipes, dropped = self.pipes[:len(self.replicas)], self.pipes[len(self.replicas):]
+        for c in dropped:
+            c.close()
+        return self.replicas
 
     def run(self) -> dict:
         kinds = set()
@@ -235,13 +274,15 @@ class Ensemble:
         n = sum(r[1] for r in res)
         el = max(r[2] for r in res)
         kind = kinds.pop() if len(kinds) == 1 else "mixed"
-        return {"value": n / el, "unit": "accesses/s", "cores": self.workers, "kind": kind,
+        self.delays = {r[3]: np.frombuffer(r[4], dtype=np.int32) for r in res}
+        nw = len(self.pipes)
+        return {"value": n / el, "unit": "accesses/s", "cores": nw, "kind": kind,
                 "cpu_model": cpu_model(),
-                "sample": f"{self.workers} processes, one per host core of this job's share, each the "
+                "sample": f"{nw} processes, one per host core of this job's share, each the "
                           f"{'reference uncore compiled from /root/reference/src' if kind == 'reference' else kind} "
-                          f"on GPU replica w's C4 stream (w = 0..{self.workers - 1}) after an untimed "
-                          f"{self.fill}-request fill, run concurrently for {self.budget:g} s: {n} requests in "
-                          f"{el:.2f} s (wall {wall:.2f} s)",
+                          f"on one GPU replica's C4 stream (replicas {self.replicas[0]}..{self.replicas[-1]}, spread "
+                          f"over the GPU's replicas) after an untimed {self.fill}-request fill, run concurrently for "
+                          f"{self.budget:g} s: {n} requests in {el:.2f} s (wall {wall:.2f} s)",
                 "per_process_accesses_per_s": [r[1] / r[2] for r in res]}
 
 
@@ -253,7 +294,13 @@ class Pass:
         self.__dict__.update(kw)
 
 
-def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, steps: int, keep_rep0: bool):
+def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, steps: int, keep: list,
+             slots: int = 0):
+    """Warm every replica, then time `steps` launches.  `keep`: replicas whose
+    delays (warmup and timed window) are returned for parity checks.  With
+    slots < R the timed launches run the replica pool (pu_run_device_pool):
+    `slots` wavefronts, each taking the next unstarted replica once its own is
+    done or halted."""
     import torch
     import torch.distributed as dist
 
@@ -271,7 +318,7 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
     gens = [P.StreamSet(specs[g:g + G]) for g in range(0, R, G)]
     host = np.zeros((G, args.chunk), dtype=A.REQ_DTYPE)
     offs = torch.from_numpy((np.arange(R + 1, dtype=np.uint64) * np.uint64(args.chunk)).view(np.int64)).to(dev)
-    rep0 = []
+    kept = {r: [] for r in keep}
 
     def next_chunk() -> torch.Tensor:
         out = torch.empty((R, args.chunk * REQ_BYTES), dtype=torch.uint8, device=dev)
@@ -288,8 +335,8 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
         d_req = next_chunk()
         um.run_device(d_req.data_ptr(), offs.data_ptr(), d_warm_delay.data_ptr(), sptr)
         torch.cuda.synchronize(dev)
-        if keep_rep0:
-            rep0.append(d_warm_delay[:args.chunk].cpu().numpy())
+        for r in keep:
+            kept[r].append(d_warm_delay[r * args.chunk:(r + 1) * args.chunk].cpu().numpy())
         del d_req
         log(f"[bench] {'closed' if replay else 'open'}-loop warmup step {s} done ({time.time() - t_w:.1f}s)")
     if os.environ.get("PU_PROF_RESET_AFTER_WARMUP"):   # tools/prof_regions.py: count the timed steps only
@@ -307,8 +354,11 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
     d_pos = torch.from_numpy(win_off[:-1].copy().view(np.int64)).to(dev)
     step_offs = [torch.from_numpy(np.concatenate([[0], win_off[:-1] + np.uint64((k + 1) * args.chunk)])
                                   .astype(np.uint64).view(np.int64)).to(dev) for k in range(steps)]
+    pool = 0 < slots < R and args.slice_ms > 0
+    d_sched = torch.zeros(um.pool_words(slots) if pool else 1, dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
-    log(f"[bench] timed requests resident: {R} x {W_t} in {time.time() - t_gen:.1f}s")
+    log(f"[bench] timed requests resident: {R} x {W_t} in {time.time() - t_gen:.1f}s"
+        + (f"; replica pool: {slots} wavefronts over {R} replicas" if pool else ""))
     before = sum_stats(um, R)
     per_before = [um.stats(r).as_dict() for r in range(R)] if os.environ.get("PU_PROF_RESET_AFTER_WARMUP") else None
 
@@ -320,7 +370,10 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
     t0 = time.perf_counter()
     for k in range(steps):
         ev[k][0].record(stream)
-        if args.slice_ms > 0:
+        if pool:
+            um.run_device_pool(d_win.data_ptr(), d_win_off.data_ptr(), d_win_delay.data_ptr(), d_pos.data_ptr(),
+                               d_sched.data_ptr(), slots, int(args.slice_ms * 1000), sptr)
+        elif args.slice_ms > 0:
             um.run_device_sliced(d_win.data_ptr(), d_win_off.data_ptr(), d_win_delay.data_ptr(), d_pos.data_ptr(),
                                  int(args.slice_ms * 1000), sptr)
         else:
@@ -335,10 +388,23 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
     log(f"[bench] timed {steps} steps in {elapsed:.3f}s; per-launch ms {['%.1f' % x for x in kern_ms]}")
     pos = d_pos.cpu().numpy().view(np.uint64)
     adv = (pos - win_off[:-1]).astype(np.int64)
+    flags = um.error_flags(R)
+    halted_mask = (flags & A.PU_ERRF_NEG_DELAY) != 0
+    pool_info = None
+    if pool:
+        sch = d_sched.cpu().numpy().view(np.uint32)
+        busy_s = float(sch[2 + slots:2 + 2 * slots].astype(np.float64).sum()) * 1e-8   # 100-MHz ticks
+        started = int(min(int(sch[0]), R))
+        pool_info = {"wavefronts": slots, "replicas": R, "replicas_started": started,
+                     "busy_fraction": busy_s / (slots * sum(kern_ms) / 1e3),
+                     "note": "every wavefront's resident time (s_memrealtime) summed over the timed launches / "
+                             "(wavefronts x the launches' HIP-event time)"}
+        log(f"[bench] replica pool: {started} of {R} replicas started, busy fraction {pool_info['busy_fraction']:.4f}")
     log(f"[bench] requests per replica in the timed window: min {adv.min()} median {int(np.median(adv))} "
-        f"max {adv.max()} of {W_t}; {int((adv >= W_t).sum())} at the end (halted replicas skip to it)")
-    if keep_rep0:
-        rep0.append(d_win_delay[:int(adv[0])].cpu().numpy())
+        f"max {adv.max()} of {W_t}; {int(((adv >= W_t) & ~halted_mask).sum())} finished the window, "
+        f"{int(halted_mask.sum())} halted (prime.cpp:130-134)")
+    for r in keep:
+        kept[r].append(d_win_delay[r * W_t:r * W_t + int(adv[r])].cpu().numpy())
     after = sum_stats(um, R)
     per_replica = None
     if per_before is not None:
@@ -347,12 +413,11 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
                 "total_num_broadcast", "L0_miss", "directory_ins", "directory_miss", "net_total_delay")
         per_replica = {k: [int(per_after[r][k] - per_before[r][k]) for r in range(R)] for k in keys}
     delta = {k: after[k] - before.get(k, 0) for k in after if k != "error_flags"}
-    flags = um.error_flags(R)
-    halted = int(((flags & A.PU_ERRF_NEG_DELAY) != 0).sum())
+    halted = int(halted_mask.sum())
     del d_win, d_win_delay
-    return Pass(elapsed=elapsed, kern_ms=kern_ms, adv=adv, rep0=rep0, delta=delta, halted=halted,
-                errf=int(np.bitwise_or.reduce(flags)) if len(flags) else 0, per_replica=per_replica,
-                steps=steps, processed=int(delta["requests"]))
+    return Pass(elapsed=elapsed, kern_ms=kern_ms, adv=adv, kept={r: np.concatenate(v) for r, v in kept.items()},
+                delta=delta, halted=halted, errf=int(np.bitwise_or.reduce(flags)) if len(flags) else 0,
+                per_replica=per_replica, steps=steps, processed=int(delta["requests"]), pool=pool_info)
 
 
 def single_instance(cfg, args, dev, threads, replay: int = 0) -> dict:
@@ -450,6 +515,8 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=10, help="timed steps")
     ap.add_argument("--warmup", type=int, default=10, help="untimed steps of --chunk requests per replica")
     ap.add_argument("--replicas", type=int, default=0, help="replicas per GPU (0 = size to HBM)")
+    ap.add_argument("--spare-replicas", type=float, default=0.1,
+                    help="replicas beyond the resident wavefront slots, as a fraction of them (replica pool)")
     ap.add_argument("--chunk", type=int, default=40960, help="requests per replica per step")
     ap.add_argument("--slice-ms", type=float, default=400.0,
                     help="timed steps are wall-time slices: every replica continues its own stream for this long "
@@ -488,12 +555,17 @@ class Device:
         share = int(os.environ.get("LOCAL_WORLD_SIZE", "1")) if "PU_BENCH_DEVICE" in os.environ else 1
         per_bytes = rbytes + (args.steps + 1) * args.chunk * (REQ_BYTES + 4)
         free, _ = torch.cuda.mem_get_info(self.dev)
-        # as many replicas as fit in HBM, but no more than the kernel keeps resident
-        # (one wave each): a time-sliced launch over more would run in two rounds
-        R = args.replicas or max(1, min(resident // share, int((free * 0.88 / share) // per_bytes)))
+        # one wavefront per replica slot the kernel keeps resident, and up to
+        # --spare-replicas more replicas (as HBM allows) for the replica pool:
+        # a wavefront whose replica halts or finishes its window takes an
+        # unstarted one (pu_run_device_pool), so no slot idles
+        res = max(1, resident // share)
+        fit = int((free * 0.88 / share) // per_bytes)
+        R = args.replicas or max(1, min(int(res * (1.0 + args.spare_replicas)), fit))
         R = max(1, R - R % 8) if R >= 8 else R
+        self.slots = min(R, res)
         log(f"[bench] rank {rank}: replica {rbytes / 2**20:.0f} MiB + requests {(per_bytes - rbytes) / 2**20:.0f} MiB, "
-            f"{R} replicas (resident limit {resident}), free {free / 2**30:.0f} GiB")
+            f"{R} replicas on {self.slots} wavefronts (resident limit {resident}), free {free / 2**30:.0f} GiB")
         self.R = R
         self.um = P.UncoreManager()
         self.um.init(cfg, replicas=R, device=local)
@@ -503,11 +575,11 @@ class Device:
         assert self.stream.cuda_stream != 0
         self.compiled = P.uncore.lib().pu_compiled_config(self.um._handle())   # 0, 1 or 2 (primeuncore.h)
 
-    def headline(self, args, rank: int, world: int):
+    def headline(self, args, rank: int, world: int, keep: list):
         import primesim_amd as P
         mode = P.uncore.PU_REPLAY_CLOSED if args.replay == "closed" else P.uncore.PU_REPLAY_OPEN
-        return run_pass(self.um, args, self.R, rank, world, self.dev, self.stream, mode, args.steps,
-                        keep_rep0=rank == 0)
+        return run_pass(self.um, args, self.R, rank, world, self.dev, self.stream, mode, args.steps, keep,
+                        self.slots)
 
     def reduce_device(self, args):
         """Where the max/sum reduction's tensors live: the GPU under RCCL."""
@@ -554,12 +626,16 @@ def main(argv=None) -> None:
     R, um, dev, stream = D.R, D.um, D.dev, D.stream
     global LAST_REPLICAS, LAST_PER_REPLICA
     LAST_REPLICAS = R
+    # the ensemble's replicas, spread over 0..R-1: their delays are checked
+    # against the reference's bit for bit (replica 0 also by cpu_baseline)
+    keep = sorted(set(ens.assign(R)) | {0}) if ens is not None else ([0] if rank == 0 else [])
 
     # ---- headline: open-loop replay
-    H = D.headline(args, rank, world)
+    H = D.headline(args, rank, world, keep)
     LAST_PER_REPLICA = H.per_replica
     t_max, tot_processed = reduce_run(H.elapsed, H.processed, D.reduce_device(args))
     _, tot_replicas = reduce_run(0.0, R, D.reduce_device(args))
+    _, tot_slots = reduce_run(0.0, D.slots, D.reduce_device(args))
     value = tot_processed / t_max
     avg_ms = float(np.mean(H.kern_ms))
     bytes_per_launch = alg_bytes(H.delta, cfg) / args.steps
@@ -569,21 +645,39 @@ def main(argv=None) -> None:
     result = None
     if rank == 0:
         ens_res = ens.run() if ens is not None else None
+        replica_parity = None
         if ens_res:
             log(f"[bench] cpu ensemble ({ens_res['kind']}, {ens_res['cores']} processes): "
                 f"{ens_res['value']:.0f} accesses/s")
+            per = {}
+            for r, d_cpu in ens.delays.items():
+                g = H.kept[r]
+                m = min(len(g), len(d_cpu))
+                per[str(r)] = {"requests_compared": m, "gpu_window_requests": int(H.adv[r]),
+                               "bit_identical": bool(np.array_equal(g[:m], d_cpu[:m]))}
+            replica_parity = {"replicas": sorted(ens.delays), "count": len(per),
+                              "requests_compared": sum(v["requests_compared"] for v in per.values()),
+                              "bit_identical": all(v["bit_identical"] for v in per.values()),
+                              "per_replica": per,
+                              "note": f"GPU delays of each replica (its {args.warmup * args.chunk}-request warmup, "
+                                      f"then its timed window) against the {ens_res['kind']} uncore's on the same "
+                                      f"stream, run by the ensemble processes, compared over the requests both ran"}
+            parity_ok &= replica_parity["bit_identical"]
+            log(f"[bench] replica parity: {replica_parity['count']} replicas "
+                f"({replica_parity['replicas'][0]}..{replica_parity['replicas'][-1]}), "
+                f"{replica_parity['requests_compared']} delays, bit-identical {replica_parity['bit_identical']}")
         closed = None
         if extras and args.closed_steps > 0:
             um.reset()
             C = run_pass(um, args, R, rank, world, dev, stream, P.uncore.PU_REPLAY_CLOSED, args.closed_steps,
-                         keep_rep0=True)
+                         [0], D.slots)
             c_par, c_cpu = None, None
             if not args.no_cpu:
                 import oracle as O
                 w0, n_t = args.warmup * args.chunk, args.closed_steps * args.chunk
                 s0 = P.generate_stream(stream_spec(replica_seed(SEED_BASE, 0, 0), w0 + n_t))
                 kind, n_cpu, el, d_cpu = cpu_baseline(xml_path, cfg, s0, threads, w0, 5.0, O.MODE_CLOSED)
-                gd = np.concatenate(C.rep0)
+                gd = C.kept[0]
                 m = min(len(d_cpu), len(gd))
                 c_par = {"kind": kind, "requests_compared": m, "bit_identical": bool(np.array_equal(gd[:m], d_cpu[:m]))}
                 parity_ok &= c_par["bit_identical"]
@@ -594,14 +688,15 @@ def main(argv=None) -> None:
                                    f"{el:.1f} s"}
                 log(f"[bench] closed-loop cpu baseline ({kind}): {n_cpu / el:.0f} accesses/s")
             closed = {"value": C.processed / C.elapsed, "unit": "accesses/s", "steps": C.steps,
-                      "per_simulation_accesses_per_s": C.processed / C.elapsed / R,
+                      "per_simulation_accesses_per_s": C.processed / C.elapsed / D.slots,
+                      "replica_pool": C.pool,
                       "halted_replicas": C.halted,
                       "mg1_share_of_link_visits": C.delta["mg1_calls"] / max(1, C.delta["net_distance"]),
                       "mean_delay_cycles": 0.0,
                       "parity": c_par,
                       "cpu_baseline": c_cpu,
                       "single_instance": None}
-            gd = np.concatenate(C.rep0)
+            gd = C.kept[0]
             closed["mean_delay_cycles"] = float(gd[gd != 0].mean()) if (gd != 0).any() else 0.0
             log(f"[bench] closed loop: {closed['value']:.4g} accesses/s, halted {C.halted}, "
                 f"M/G/1 share {closed['mg1_share_of_link_visits']:.3f}")
@@ -620,7 +715,7 @@ def main(argv=None) -> None:
             w0, n_t = args.warmup * args.chunk, args.steps * args.chunk
             s0 = P.generate_stream(stream_spec(replica_seed(SEED_BASE, rank, 0), w0 + n_t))
             kind, n_cpu, el, d_cpu = cpu_baseline(xml_path, cfg, s0, threads, w0, args.cpu_seconds)
-            gpu_d = np.concatenate(H.rep0)
+            gpu_d = H.kept[0]
             m = min(len(d_cpu), len(gpu_d))
             parity = bool(np.array_equal(gpu_d[:m], d_cpu[:m]))
             parity_ok &= parity
@@ -641,9 +736,14 @@ def main(argv=None) -> None:
             built = P.uncore.library_source_hash()
             if tj.get("src_hash") == built:
                 traffic = tj["fabric_bytes_per_access"] * (H.processed / args.steps)
+                how = ("reads in 32-B units (TCC_EA0_RDREQ_*_32B) + WRITE_SIZE" if "read_bytes_per_launch_32b_units" in tj
+                       else "FETCH_SIZE+WRITE_SIZE")
+                win = " ".join(tj.get("bench_args", [])[:4])
                 traffic_src = (f"{os.path.relpath(args.traffic_json, ROOT)}: {tj['fabric_bytes_per_access']:.0f} B/access "
-                               f"(FETCH_SIZE+WRITE_SIZE, separate PMC passes; fabric bytes incl. MALL hits) measured "
-                               f"on build {built} at {tj['replicas']} replicas")
+                               f"({how}, separate PMC passes; fabric bytes incl. MALL hits) measured on build {built} "
+                               f"at {tj['replicas']} replicas, bench window {win}; "
+                               f"{tj['fabric_bytes_per_access'] / max(1e-9, alg_bytes(H.delta, cfg) / H.processed):.2f}x "
+                               f"this run's algorithmic bytes per access")
             else:
                 traffic_src = (f"not reported: {os.path.relpath(args.traffic_json, ROOT)} was measured on build "
                                f"{tj.get('src_hash')}, this library is {built}")
@@ -665,22 +765,25 @@ def main(argv=None) -> None:
                             "directory MESI full-map, uniform 2^20 lines + 64-line hotspot, 25% writes, open-loop replay",
                 "replicas_per_gpu": R,
                 "replicas_total": tot_replicas,
+                "wavefronts_per_gpu": D.slots,
+                "replica_pool": H.pool,
                 "step": (f"wall-time slice: every replica continues its own stream for {args.slice_ms:g} ms per "
                          f"launch, stopping only between requests" if args.slice_ms > 0 else
                          f"fixed: {args.chunk} requests per replica per launch"),
                 "mean_requests_per_replica_per_step": H.processed / (R * args.steps),
                 "warmup_requests_per_replica": args.warmup * args.chunk,
-                "parallelism": (f"replicas: {R} independent uncores per GPU x {world} GPU(s), one process per GPU, "
-                                f"no data-path collective ({args.dist_backend} for the barrier and the max/sum "
-                                f"reduction only)" if world > 1 else
-                                f"replicas: {R} independent uncores on 1 GPU"),
+                "parallelism": (f"replicas: {R} independent uncores per GPU ({D.slots} simulated at once, one "
+                                f"wavefront each) x {world} GPU(s), one process per GPU, no data-path collective "
+                                f"({args.dist_backend} for the barrier and the max/sum reduction only)" if world > 1 else
+                                f"replicas: {R} independent uncores on 1 GPU, {D.slots} simulated at once (one "
+                                f"wavefront each)"),
                 "halted_replicas": H.halted,
                 "mg1_share_of_link_visits": H.delta["mg1_calls"] / max(1, H.delta["net_distance"]),
                 "error_flags": H.errf & ~A.PU_ERRF_NEG_DELAY,
                 "engine_build": P.uncore.library_source_hash(),
                 "engine_variant": VARIANTS[D.compiled],
             },
-            "per_simulation_accesses_per_s": value / tot_replicas,
+            "per_simulation_accesses_per_s": value / tot_slots,
             "single_instance": single,
             "closed_loop": closed,
             "roofline": {
@@ -691,13 +794,15 @@ def main(argv=None) -> None:
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": "pu_jit_uncore_s1_h0" if D.compiled == 2 else "uncore_kernel<1, true, false>",
+                "kernel": (("pu_jit_uncore_s2_h0" if H.pool else "pu_jit_uncore_s1_h0") if D.compiled == 2 else
+                           ("uncore_kernel<1, 2, false>" if H.pool else "uncore_kernel<1, 1, false>")),
                 "avg_launch_ms": avg_ms,
                 "alg_bytes_per_launch": bytes_per_launch,
                 "limiter": LIMITER,
             },
             "cpu_baseline": cpu,
             "cpu_baseline_ensemble": ens_res,
+            "replica_parity": replica_parity,
             "parity": parity_ok if (not args.no_cpu and world == 1) else None,
         }
         print(json.dumps(result), flush=True)

@@ -249,6 +249,10 @@ long pu_config_geo_source(const pu_sim_cfg* cfg, char* buf, size_t cap);
  * 0 the ahead-of-time kernels only. */
 int pu_config_jit_warm(const pu_sim_cfg* cfg);
 int pu_compiled_config(const pu_handle* h);
+/* The 8-hex-digit tag of the engine sources this library compiles: the prefix
+ * of every code object it writes to the cache (cache maintenance keeps the
+ * code objects whose prefix some library still carries). */
+const char* pu_jit_source_tag(void);
 /* Return all replicas to the just-initialised state (no reallocation). */
 int        pu_reset(pu_handle* h);
 int        pu_num_replicas(const pu_handle* h);
@@ -338,6 +342,26 @@ int pu_run_device(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off,
  * same as one unsliced run over the same requests.  budget_us = 0: no limit. */
 int pu_run_device_sliced(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off,
                          int32_t* d_delay, uint64_t* d_pos, uint64_t budget_us, void* hip_stream);
+/* Replica pool: pu_run_device_sliced for more replicas than run at once (no
+ * reference counterpart; throughput runs).  A launch runs `slots` wavefronts,
+ * 1 <= slots <= pu_pool_slots(h) = min(num_replicas, pu_resident_replicas).
+ * Each slot continues the replica it held when the previous pool launch
+ * ended; a slot whose replica is done (d_pos[r] reached d_off[r+1], or the
+ * replica stopped by the prime.cpp:130-134 rule: the rest of its range reads
+ * 0) takes the next replica nobody has started, in index order, and goes on
+ * within the same slice, so no wavefront idles while unstarted replicas
+ * remain.  Per replica the results are those of pu_run_device_sliced (each
+ * replica is processed in order, by one wavefront at a time).  d_sched:
+ * pu_pool_words(slots) = 2 + 2*slots uint32 words of device memory, all 0
+ * before the first launch of a pool run, the same slots for every launch of
+ * it (word 0 = replicas taken so far; word 1 unused; then per slot its
+ * replica + 1, then per slot the 100-MHz ticks its wavefronts have been
+ * resident, summed over launches: the busy time of the pool).
+ * budget_us > 0. */
+int  pu_pool_slots(pu_handle* h);
+long pu_pool_words(int slots);
+int  pu_run_device_pool(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
+                        uint64_t* d_pos, uint32_t* d_sched, int slots, uint64_t budget_us, void* hip_stream);
 int pu_synchronize(pu_handle* h);
 
 /* Per-core completion cycle of the last request each core issued

@@ -612,15 +612,21 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
 // those change only when the link is visited.  In latency mode a second wave
 // of the workgroup (mg1_helper) recomputes the wait of every link a route
 // window just updated, on another SIMD, and stores it as
-// d.x = wait | (n mod 2^24) << 40; the simulating wave uses it when the tag
-// matches its header's n and computes the wait itself otherwise.  The main
-// wave writes piece a (which holds n) after b and c; the helper reads a
-// first: a wait it stores was computed from moments at least as new as its
-// tag says, so any newer moments carry another n and the tag cannot match.
+// d.x = wait | (n ^ wait) << 32 (n < 2^32, waits < 2^32 - 1; larger ones
+// are not cached); the simulating wave uses it when the high half xor the
+// wait equals its header's n and computes the wait itself otherwise.  The tag
+// is n itself, not a residue, so a slot the helper skipped (it fell more than
+// PU_HQ ids behind) can never match a later visit; folding the wait into it
+// makes a read of the slot torn against the helper's write (old wait, new tag
+// or the reverse) fail the check unless both waits are equal.  The main wave writes piece a (which holds n) after b
+// and c; the helper reads a, then b, then a again and stores only when both
+// reads of a are bit-identical (Σs grows at every visit, so a read of a torn
+// against the main wave's write, or a b newer than a, shows as a mismatch):
+// a stored wait was computed from exactly the moments its tag names.
 #define PU_LDS_QHDR_BYTES (136 * 1024)
 #define PU_LDS_SLOT 4u                     // 16-B pieces per LDS header slot
 #define PU_MG1_CACHE_NONE 0xFFFFFFFFFFFFFFFFull
-#define PU_MG1_WAIT_BITS 40
+#define PU_MG1_WAIT_BITS 32
 #define AS3 __attribute__((address_space(3)))
 static __shared__ v4u32 lds_qhdr[PU_LDS_QHDR_BYTES / 16];
 // queue ids whose header the main wave just wrote back, for the helper
@@ -920,7 +926,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         if constexpr (LH) {
             const uint64_t wmask = (1ull << PU_MG1_WAIT_BITS) - 1;
             const bool hit = need && (vcache & wmask) != wmask && hs.n < 4294967296.0 &&
-                             (uint32_t)(vcache >> PU_MG1_WAIT_BITS) == ((uint32_t)hs.n & 0xFFFFFFu);
+                             ((uint32_t)(vcache >> PU_MG1_WAIT_BITS) ^ (uint32_t)vcache) == (uint32_t)hs.n;
             if (hit) vd = vcache & wmask;
             need = need && !hit;
         }
@@ -1090,8 +1096,9 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
 
 // Latency mode, the workgroup's second wave: recompute the M/G/1 wait of every
 // link the simulating wave publishes (lds_hq), from the moments in the LDS
-// header image, and store it in the link's cache slot tagged with n mod 2^24.
-// Reads piece a (n) before b and c (the main wave writes it after them).
+// header image, and store it in the link's cache slot tagged with n.  Reads
+// piece a (n), then b, then a again (the main wave writes a after b and c)
+// and stores only when the two reads of a agree.
 // Returns once the main wave has left its loop and every id is processed.
 __device__ void mg1_helper() {
     const int ln = lane_id();
@@ -1114,13 +1121,16 @@ __device__ void mg1_helper() {
             const v4u32 a = H[0];
             asm volatile("" ::: "memory");
             const v4u32 b = H[1];
+            asm volatile("" ::: "memory");
+            const v4u32 a2 = H[0];
             const QState st = hdr_state(a, b, v4u32{0u, 0u, 0u, 0u});   // M/G/1 needs a and b only
             const uint64_t w = mg1_wait(st);
             const uint64_t wmask = (1ull << PU_MG1_WAIT_BITS) - 1;
-            const bool st_ok = w < wmask && st.n < 4294967296.0;
+            const bool same = a.x == a2.x && a.y == a2.y && a.z == a2.z && a.w == a2.w;
+            const bool st_ok = same && w < wmask && st.n < 4294967296.0;
             if (st_ok)
                 *(volatile AS3 uint64_t*)&lds_qhdr[(size_t)q * PU_LDS_SLOT + 3] =
-                    w | ((uint64_t)((uint32_t)st.n & 0xFFFFFFu) << PU_MG1_WAIT_BITS);
+                    w | ((uint64_t)((uint32_t)st.n ^ (uint32_t)w) << PU_MG1_WAIT_BITS);
 #ifdef PU_PROF
             const uint64_t nst = __builtin_popcountll(ballot(st_ok));
             if (ln == 0) atomicAdd(&lds_prof[PF_MG1STORED], (unsigned long long)nst);
@@ -2202,68 +2212,44 @@ __device__ __forceinline__ void stats_init() {
     __syncthreads();
 }
 
-// One workgroup (= one wavefront) per replica.  Replica replica0 + blockIdx.x
-// processes reqs[off[blockIdx.x] .. off[blockIdx.x+1]) in order: the message
-// loop of prime.cpp:120-137 (D restarts at each batch_start; d = access(core,
-// req, timer + D); D += d - 1).
-//
-// Time-sliced launches (pos != nullptr): replica r starts at pos[r] instead of
-// off[r], stops before the first request that would begin after
-// `budget_ticks` of the s_memrealtime clock (100 MHz) have passed since the
-// wave started, and writes its next position back to pos[r].  A replica only
-// ever stops between requests, so its stream continues exactly in the next
-// launch; the slice keeps every wave busy instead of waiting for the slowest
-// replica of a fixed-size step.
-// SLICED is a separate instantiation so profiles list the time-sliced launches
-// (uncore_kernel<NL, true>) apart from fixed-range ones.
+// A replica-pool wave's own state (uncore_body), in LDS: lane 0 writes it.
+struct PoolCtl {
+    uint32_t* sched;
+    char* arena;
+    int32_t nrep;
+    int32_t r;            // the replica the wave holds, -1 = none
+};
+static __shared__ PoolCtl lds_pool;
+// The replica a pool wave runs next: `cur` if it holds one, else the next
+// unstarted replica (sched[0], one device-scope atomic by lane 0); -1 once
+// every replica has been taken.
+__device__ __forceinline__ int pool_next(int cur) {
+    if (cur >= 0) return cur;
+    uint32_t t = 0;
+    if (lane_id() == 0) t = __hip_atomic_fetch_add(&lds_pool.sched[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int r = (int)rl32(t, 0);
+    return r < (int)uni32((uint32_t)lds_pool.nrep) ? r : -1;
+}
+
+// One replica's message loop (prime.cpp:120-137): reqs[b .. end) in order, D
+// restarting at each batch_start; d = access(core, req, timer + D); D += d - 1.
+// e.base is the replica's arena.  Time-sliced launches (deadline != MAX) stop
+// before the first request that would begin at or after `deadline`
+// (s_memrealtime, 100 MHz); a replica only ever stops between requests, so
+// its stream continues exactly in the next launch.  The index of the first
+// request not processed goes to *pos_out (if given); returns whether the
+// range is done.
 template <int NL, bool SLICED, bool LH>
-__device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __restrict__ arena, int replica0,
-                                            const pu_req* __restrict__ reqs, const uint64_t* __restrict__ off,
-                                            int32_t* __restrict__ delays, uint64_t* __restrict__ pos,
-                                            uint64_t budget_ticks, uint32_t flags) {
-    if constexpr (!SLICED) {
-        pos = nullptr;
-        budget_ticks = 0;
-    }
-    const uint64_t wave_t0 = __builtin_amdgcn_s_memrealtime();
-    Engine<NL, LH> e;
-    e.g = g;
-    e.ln = lane_id();
-    e.base = arena + (size_t)(replica0 + (int)blockIdx.x) * e.g->replica_bytes;
-    if constexpr (LH) {
-        // Latency mode: a two-wave workgroup.  Both waves copy the replica's
-        // queue headers into the LDS image (pieces a, b, c; d = no cached
-        // wait); wave 0 simulates, wave 1 is the M/G/1 helper (mg1_helper).
-        const AS1 v4u32* gh = (const AS1 v4u32*)(AS1 char*)(e.base + OFF(e.g->off_qhdr));
-        const uint32_t nq4 = (uint32_t)e.g->nqueues * PU_LDS_SLOT;
-        for (uint32_t k = threadIdx.x; k < nq4; k += 128)
-            lds_qhdr[k] = (k & 3u) < 3u ? gh[(k >> 2) * PU_HDR_PIECES + (k & 3u)] : v4u32{~0u, ~0u, 0u, 0u};
-        if (threadIdx.x == 0) {
-            lds_hq_head = 0;
-            lds_main_done = 0;
-        }
-        if (threadIdx.x >= 64) {                          // the helper wave
-            __syncthreads();                              // [1] stats_init's
-            mg1_helper();
-            __syncthreads();                              // [2] the main wave left its loop
-            AS1 v4u32* gho = (AS1 v4u32*)(AS1 char*)(e.base + OFF(e.g->off_qhdr));
-            for (uint32_t k = threadIdx.x; k < nq4; k += 128)
-                if ((k & 3u) < 3u) gho[(k >> 2) * PU_HDR_PIECES + (k & 3u)] = lds_qhdr[k];
-            __syncthreads();                              // [3] before the stats flush
-            return;
-        }
-    }
+__device__ __forceinline__ bool replica_loop(Engine<NL, LH>& e, const pu_req* __restrict__ reqs,
+                                             int32_t* __restrict__ delays, uint64_t b, uint64_t end,
+                                             uint64_t* __restrict__ pos_out, uint64_t deadline, uint32_t flags) {
     e.hq_head = 0;
     stats_init();
     e.dly = 0;
     e.hit = false;
-#ifdef PU_PROF
-    const uint64_t blk_t0 = __builtin_amdgcn_s_memrealtime();
-#endif
-
     // The message loop's own state lives in LDS (lane 0 writes, every lane reads
     // it back wave-uniform): nothing of it stays in registers across the
-    // inlined access(), whose register budget is tight (4 waves/SIMD).
+    // inlined access(), whose register budget is tight (5 waves/SIMD).
     RunState* rs = e.template at<RunState>(OFF(e.g->off_run));
     if (e.ln == 0) {
         const int32_t h0 = rs->halted;
@@ -2274,7 +2260,7 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
         lds_ctl.flags = flags;
         lds_ctl.msg_shift = rs->msg_shift;
         lds_ctl.dead_tags = rs->dead_tags;
-        lds_ctl.deadline = budget_ticks ? wave_t0 + budget_ticks : UINT64_MAX;
+        lds_ctl.deadline = deadline;
         lds_ctl.done = 0;
         lds_ctl.cur = 0;
         lds_ctl.limit_at = UINT64_MAX;
@@ -2282,14 +2268,10 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
     __builtin_amdgcn_wave_barrier();
     e.init_shared((int32_t)rl32(e.ln == 0 ? (uint32_t)rs->pool_top : 0u, 0), rl64(e.ln == 0 ? rs->page_next : 0ull, 0),
                   rl64(e.ln == 0 ? rs->last_addr : 0ull, 0));
-    const uint64_t b = pos ? pos[blockIdx.x] : off[blockIdx.x], end = off[blockIdx.x + 1];
     uint64_t i = b;
     for (; i < end; i++) {
         if (SLICED && __builtin_amdgcn_s_memrealtime() >= uni64(lds_ctl.deadline)) break;
-        if (uni32((uint32_t)lds_ctl.halted)) {   // the reference's handler thread has exited
-            if (e.ln == 0) delays[i] = 0;
-            continue;
-        }
+        if (uni32((uint32_t)lds_ctl.halted)) break;   // the rest is zero-filled below
         PROF_T(p_loop);
         const pu_req q = reqs[i];
         const bool core_ok = q.core >= 0 && q.core < e.g->num_cores;
@@ -2338,17 +2320,24 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
         __builtin_amdgcn_wave_barrier();
         PROF_ADD(PF_LOOP, p_loop);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no staging DMA outlives the wave
-    if constexpr (LH) {                                   // ... and the headers back
-        if (e.ln == 0) *(volatile AS3 uint32_t*)&lds_main_done = 1u;
-        __syncthreads();                                  // [2]
-        AS1 v4u32* gh = (AS1 v4u32*)(AS1 char*)(e.base + OFF(e.g->off_qhdr));
-        const uint32_t nq4 = (uint32_t)e.g->nqueues * PU_LDS_SLOT;
-        for (uint32_t k = threadIdx.x; k < nq4; k += 128)
-            if ((k & 3u) < 3u) gh[(k >> 2) * PU_HDR_PIECES + (k & 3u)] = lds_qhdr[k];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no staging DMA outlives the loop
+    if (i < end && uni32((uint32_t)lds_ctl.halted)) {
+        // the reference's handler thread has exited (prime.cpp:130-134):
+        // nothing more is simulated; the rest of the range reads 0, written
+        // by the whole wave at once
+        for (uint64_t k = i + (uint64_t)e.ln; k < end; k += 64) delays[k] = 0;
+        i = end;
     }
+    if (pos_out && e.ln == 0) *pos_out = i;
+    return i >= end;
+}
+
+// The replica's run state back to HBM and its counters flushed, after
+// replica_loop (and, in latency mode, after the header image went back).
+template <int NL, bool LH>
+__device__ __forceinline__ void replica_close(Engine<NL, LH>& e) {
+    RunState* rs = e.template at<RunState>(OFF(e.g->off_run));
     if (e.ln == 0) {
-        if (pos) pos[blockIdx.x] = i;
         rs->batch_delay = lds_ctl.D;
         rs->halted = (lds_ctl.flags & PU_KF_NOHALT) ? (lds_ctl.halted0 | lds_ctl.halted) : lds_ctl.halted;
         rs->skip_msg = lds_ctl.skip;
@@ -2364,22 +2353,138 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
     e.flush_stats();
 #ifdef PU_PROF
     if (e.ln < PF_COUNT) atomicAdd(&g_prof[e.ln], lds_prof[e.ln]);
-    if (e.ln == 0 && blockIdx.x < PU_PROF_BLOCKS) {
-        const uint64_t blk_t1 = __builtin_amdgcn_s_memrealtime();
-        g_blk_t0[blockIdx.x] = blk_t0;
-        g_blk_t1[blockIdx.x] = blk_t1;
-        g_blk_dur[blockIdx.x] += blk_t1 - blk_t0;
-    }
 #endif
 }
 
+// One workgroup (= one wavefront) per replica.  Replica replica0 + blockIdx.x
+// processes reqs[off[blockIdx.x] .. off[blockIdx.x+1]) in order (replica_loop).
+//
+// Time-sliced launches (pos != nullptr): replica r starts at pos[r] instead of
+// off[r], stops before the first request that would begin after
+// `budget_ticks` of the s_memrealtime clock (100 MHz) have passed since the
+// wave started, and writes its next position back to pos[r]; the slice keeps
+// every wave busy instead of waiting for the slowest replica of a fixed-size
+// step.
+//
+// Replica pool (sched != nullptr; time-sliced throughput launches of more
+// replicas than the device keeps resident, pu_run_device_pool): the grid is
+// one wave per resident slot.  Slot w continues the replica it held when the
+// previous launch ended (sched[PU_POOL_SLOT0 + w] = replica + 1; 0 = none);
+// once that replica's range is done (its end reached, or stopped by the
+// prime.cpp:130-134 rule) the wave takes the next unstarted replica from the
+// queue (sched[0], one device-scope atomic by lane 0) and continues within
+// the same slice, so no wave idles while replicas remain.  nrep = replicas.
+// Each slot adds its wave's lifetime in s_memrealtime ticks to a counter
+// (the host's busy-time accounting).
+// MODE: 0 fixed ranges, 1 time-sliced, 2 replica pool (time-sliced); each a
+// separate instantiation, so the pool's bookkeeping costs the others nothing
+// and profiles list the launch kinds apart.
+template <int NL, int MODE, bool LH>
+__device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __restrict__ arena, int replica0,
+                                            const pu_req* __restrict__ reqs, const uint64_t* __restrict__ off,
+                                            int32_t* __restrict__ delays, uint64_t* __restrict__ pos,
+                                            uint64_t budget_ticks, uint32_t flags, uint32_t* __restrict__ sched,
+                                            int nrep) {
+    constexpr bool SLICED = MODE >= 1;
+    constexpr bool pool = MODE == 2 && !LH;
+    if constexpr (!SLICED) {
+        pos = nullptr;
+        budget_ticks = 0;
+    }
+    if constexpr (!pool) sched = nullptr;
+    const uint64_t wave_t0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t deadline = budget_ticks ? wave_t0 + budget_ticks : UINT64_MAX;
+    Engine<NL, LH> e;
+    e.g = g;
+    e.ln = lane_id();
+    // The replica this wave runs now; in a replica pool the wave's own state
+    // (the pool arguments, its replica) stays in LDS across the inlined
+    // engine, whose register budget is tight, and the one replica_loop call
+    // site below serves every replica the wave takes.
+    int r = replica0 + (int)blockIdx.x;
+    if constexpr (pool) {
+        if (e.ln == 0) {
+            lds_pool.sched = sched;
+            lds_pool.arena = arena;
+            lds_pool.nrep = nrep;
+            lds_pool.r = (int32_t)sched[PU_POOL_SLOT0 + blockIdx.x] - 1;
+        }
+        __builtin_amdgcn_wave_barrier();
+        r = pool_next((int)uni32((uint32_t)lds_pool.r));
+    }
+    while (r >= 0) {
+        if (pool && e.ln == 0) lds_pool.r = r;
+        e.base = (char*)uni64((uint64_t)(pool ? lds_pool.arena : arena)) + (size_t)r * OFF(e.g->replica_bytes);
+        if constexpr (LH) {
+            // Latency mode: a two-wave workgroup.  Both waves copy the replica's
+            // queue headers into the LDS image (pieces a, b, c; d = no cached
+            // wait); wave 0 simulates, wave 1 is the M/G/1 helper (mg1_helper).
+            const AS1 v4u32* gh = (const AS1 v4u32*)(AS1 char*)(e.base + OFF(e.g->off_qhdr));
+            const uint32_t nq4 = (uint32_t)e.g->nqueues * PU_LDS_SLOT;
+            for (uint32_t k = threadIdx.x; k < nq4; k += 128)
+                lds_qhdr[k] = (k & 3u) < 3u ? gh[(k >> 2) * PU_HDR_PIECES + (k & 3u)] : v4u32{~0u, ~0u, 0u, 0u};
+            if (threadIdx.x == 0) {
+                lds_hq_head = 0;
+                lds_main_done = 0;
+            }
+            if (threadIdx.x >= 64) {                      // the helper wave
+                __syncthreads();                          // [1] stats_init's
+                mg1_helper();
+                __syncthreads();                          // [2] the main wave left its loop
+                AS1 v4u32* gho = (AS1 v4u32*)(AS1 char*)(e.base + OFF(e.g->off_qhdr));
+                for (uint32_t k = threadIdx.x; k < nq4; k += 128)
+                    if ((k & 3u) < 3u) gho[(k >> 2) * PU_HDR_PIECES + (k & 3u)] = lds_qhdr[k];
+                __syncthreads();                          // [3] before the stats flush
+                return;
+            }
+        }
+#ifdef PU_PROF
+        const uint64_t blk_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+        // the range: off[] and pos[] are indexed by replica in a pool, by
+        // workgroup otherwise
+        const int ix = pool ? r : (int)blockIdx.x;
+        const uint64_t b = pos ? pos[ix] : off[ix], end = off[ix + 1];
+        const bool done = replica_loop<NL, SLICED, LH>(e, reqs, delays, b, end, pos ? pos + ix : nullptr, deadline,
+                                                       flags);
+        if constexpr (LH) {                               // the headers back
+            if (e.ln == 0) *(volatile AS3 uint32_t*)&lds_main_done = 1u;
+            __syncthreads();                              // [2]
+            AS1 v4u32* gh = (AS1 v4u32*)(AS1 char*)(e.base + OFF(e.g->off_qhdr));
+            const uint32_t nq4 = (uint32_t)e.g->nqueues * PU_LDS_SLOT;
+            for (uint32_t k = threadIdx.x; k < nq4; k += 128)
+                if ((k & 3u) < 3u) gh[(k >> 2) * PU_HDR_PIECES + (k & 3u)] = lds_qhdr[k];
+        }
+        replica_close<NL, LH>(e);
+#ifdef PU_PROF
+        if (e.ln == 0 && blockIdx.x < PU_PROF_BLOCKS) {
+            const uint64_t blk_t1 = __builtin_amdgcn_s_memrealtime();
+            g_blk_t0[blockIdx.x] = blk_t0;
+            g_blk_t1[blockIdx.x] = blk_t1;
+            g_blk_dur[blockIdx.x] += blk_t1 - blk_t0;
+        }
+#endif
+        if (!pool) break;
+        // a pool wave: keep the replica if the slice ran out, else take the next
+        if (!done) break;
+        r = pool_next(-1);
+        if (r < 0 && e.ln == 0) lds_pool.r = -1;
+    }
+    if (pool && e.ln == 0) {
+        uint32_t* S = lds_pool.sched;
+        S[PU_POOL_SLOT0 + blockIdx.x] = (uint32_t)(lds_pool.r + 1);
+        S[PU_POOL_SLOT0 + gridDim.x + blockIdx.x] += (uint32_t)(__builtin_amdgcn_s_memrealtime() - wave_t0);
+    }
+}
+
 #ifndef PU_JIT_GEO
-template <int NL, bool SLICED, bool LH = false>
+template <int NL, int MODE, bool LH = false>
 __global__ __launch_bounds__(LH ? 128 : 64) __attribute__((amdgpu_waves_per_eu(LH ? 1 : PU_MIN_WAVES(NL)))) void uncore_kernel(
     const Geo* __restrict__ g, char* __restrict__ arena, int replica0, const pu_req* __restrict__ reqs,
     const uint64_t* __restrict__ off, int32_t* __restrict__ delays, uint64_t* __restrict__ pos, uint64_t budget_ticks,
-    uint32_t flags) {
-    uncore_body<NL, SLICED, LH>(PU_AOT_GEO(g), arena, replica0, reqs, off, delays, pos, budget_ticks, flags);
+    uint32_t flags, uint32_t* __restrict__ sched, int nrep) {
+    uncore_body<NL, MODE, LH>(PU_AOT_GEO(g), arena, replica0, reqs, off, delays, pos, budget_ticks, flags, sched,
+                                nrep);
 }
 #else
 }  // namespace
@@ -2389,13 +2494,15 @@ __global__ __launch_bounds__(LH ? 128 : 64) __attribute__((amdgpu_waves_per_eu(L
     extern "C" __global__ __launch_bounds__(H ? 128 : 64) __attribute__((amdgpu_waves_per_eu(H ? 1 : PU_MIN_WAVES(PU_JIT_NL)))) \
     void NAME(const Geo* __restrict__ g, char* __restrict__ arena, int replica0, const pu_req* __restrict__ reqs,     \
               const uint64_t* __restrict__ off, int32_t* __restrict__ delays, uint64_t* __restrict__ pos,            \
-              uint64_t budget_ticks, uint32_t flags) {                                                               \
-        uncore_body<PU_JIT_NL, S, H>(&kJitGeo, arena, replica0, reqs, off, delays, pos, budget_ticks, flags); \
+              uint64_t budget_ticks, uint32_t flags, uint32_t* __restrict__ sched, int nrep) {                       \
+        uncore_body<PU_JIT_NL, S, H>(&kJitGeo, arena, replica0, reqs, off, delays, pos, budget_ticks, flags, sched,  \
+                                     nrep);                                                                          \
     }
-PU_JIT_KERNEL(pu_jit_uncore_s0_h0, false, false)
-PU_JIT_KERNEL(pu_jit_uncore_s0_h1, false, true)
-PU_JIT_KERNEL(pu_jit_uncore_s1_h0, true, false)
-PU_JIT_KERNEL(pu_jit_uncore_s1_h1, true, true)
+PU_JIT_KERNEL(pu_jit_uncore_s0_h0, 0, false)
+PU_JIT_KERNEL(pu_jit_uncore_s0_h1, 0, true)
+PU_JIT_KERNEL(pu_jit_uncore_s1_h0, 1, false)
+PU_JIT_KERNEL(pu_jit_uncore_s1_h1, 1, true)
+PU_JIT_KERNEL(pu_jit_uncore_s2_h0, 2, false)
 namespace {
 #endif
 
@@ -2534,14 +2641,16 @@ extern "C" int pu_engine_unit_network(const Geo* d_geo, char* base, const int32_
 // ---------------------------------------------------------------- launchers
 extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,
                                 const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
-                                uint64_t budget_ticks, uint32_t flags, int lds_headers, hipStream_t stream) {
+                                uint64_t budget_ticks, uint32_t flags, int lds_headers, uint32_t* sched, int nrep,
+                                hipStream_t stream) {
     dim3 grid((unsigned)nblocks), block(lds_headers ? 128 : 64);   // latency mode: + the M/G/1 helper wave
 #define PU_LAUNCH3(L, S, H)                                                                                        \
     hipLaunchKernelGGL((uncore_kernel<L, S, H>), grid, block, 0, stream, d_geo, arena, replica0, reqs, off, delays,   \
-                       pos, budget_ticks, flags)
+                       pos, budget_ticks, flags, sched, nrep)
 #define PU_LAUNCH(L)                                                                                              \
-    if (pos) { if (lds_headers) PU_LAUNCH3(L, true, true); else PU_LAUNCH3(L, true, false); }                     \
-    else { if (lds_headers) PU_LAUNCH3(L, false, true); else PU_LAUNCH3(L, false, false); }
+    if (sched) PU_LAUNCH3(L, 2, false);                                                                            \
+    else if (pos) { if (lds_headers) PU_LAUNCH3(L, 1, true); else PU_LAUNCH3(L, 1, false); }                      \
+    else { if (lds_headers) PU_LAUNCH3(L, 0, true); else PU_LAUNCH3(L, 0, false); }
     switch (num_levels) {
         case 1: PU_LAUNCH(1); break;
         case 2: PU_LAUNCH(2); break;
@@ -2561,10 +2670,10 @@ extern "C" int pu_engine_occupancy(int num_levels, int* blocks_per_cu) {
     int n = 0;
     hipError_t e;
     switch (num_levels) {
-        case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<1, true>, 64, 0); break;
-        case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<2, true>, 64, 0); break;
-        case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<3, true>, 64, 0); break;
-        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<4, true>, 64, 0); break;
+        case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<1, 1>, 64, 0); break;
+        case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<2, 1>, 64, 0); break;
+        case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<3, 1>, 64, 0); break;
+        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<4, 1>, 64, 0); break;
         default: return PU_EINVAL;
     }
     *blocks_per_cu = n;

@@ -181,6 +181,13 @@ struct Geo {
 };
 
 // Kernel flags (per launch).
+// Replica pool (pu_run_device_pool): the scheduling words shared by the host
+// and the kernel.  sched[0] = next unstarted replica (the queue head);
+// sched[PU_POOL_SLOT0 + w] = replica + 1 held by slot w (0 = none), then one
+// word per slot: the s_memrealtime ticks (100 MHz) its wavefronts have been
+// resident, summed over launches.  All zero = nothing started.
+#define PU_POOL_SLOT0 2u
+#define PU_POOL_WORDS(slots) (PU_POOL_SLOT0 + 2u * (uint32_t)(slots))
 #define PU_KF_NOHALT   1u   // System::access semantics: no prime.cpp:130-134 stop (pu_access)
 #define PU_KF_MSGHALT  2u   // a negative running delay stops only that message's receive
                             // thread (pu_req.tag): the rest of the message and every later

@@ -10,12 +10,16 @@
 // its configuration and the scalar address arithmetic around them, the
 // largest part of the lone wave's issue and wait time.
 //
-// Code objects are cached on disk by a hash of (sources, geometry, options):
-// PRIMEUNCORE_JIT_CACHE, else jit_cache/ next to libprimeuncore.so (in-tree,
-// so a cache warmed by __graft_entry__.build() travels with the library).
-// PRIMEUNCORE_JIT=0 turns the specialisation off: the library's ahead-of-time
-// kernels (the same engine source compiled for a runtime Geo) run instead, as
-// they do when hipRTC is unavailable or a compile fails (with a message).
+// Code objects are cached on disk as <source tag>-<hash of (sources, geometry,
+// target arch, options)>.hsaco: PRIMEUNCORE_JIT_CACHE, else jit_cache/ next to
+// libprimeuncore.so (in-tree, so a cache warmed by __graft_entry__.build()
+// travels with the library; tools/jit_warm.py prunes code objects whose source
+// tag no library in the tree carries).  A cached code object the device
+// refuses is deleted and compiled again once.  PRIMEUNCORE_JIT=0 turns the
+// specialisation off: the library's ahead-of-time kernels (the same engine
+// source compiled for a runtime Geo) run instead, as they do when a compile or
+// a load fails (with a message).  hipRTC itself is a link-time dependency of
+// the library (-lhiprtc), not an optional one.
 #include <dlfcn.h>
 #include <sys/stat.h>
 #include <utime.h>
@@ -101,14 +105,17 @@ void write_file_atomic(const std::string& path, const std::vector<char>& data) {
     if (std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
 }
 
-std::vector<std::string> options(int waves_1level) {
+std::vector<std::string> options(const std::string& arch, int waves_1level) {
     // max-occupancy: at C4 the throughput kernel spills 2 VGPRs instead of 4
     // and ran ahead of max-ILP in each of three interleaved rounds (233.0 /
     // 230.0 / 232.7 vs 215.9 / 226.9 / 231.4 M/s), one simulation alone level
-    // (profiles/r3q_ab_occ*.txt); the ahead-of-time kernels keep max-ILP
-    std::vector<std::string> o = {"--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-fwrapv",
+    // (profiles/r3q_ab_occ*.txt); the ahead-of-time kernels keep max-ILP.
+    // -Werror=missing-field-initializers: a Geo field the emitter (geo_emit.h)
+    // forgets would otherwise silently be 0 in the compiled configuration.
+    std::vector<std::string> o = {"--offload-arch=" + arch, "-O3", "-std=c++20", "-ffp-contract=off", "-fwrapv",
                                   "-mllvm", "-amdgpu-sched-strategy=max-occupancy",
-                                  "-DPU_JIT_GEO=\"pu_jit_geo.h\"", "-Wno-c99-designator"};
+                                  "-DPU_JIT_GEO=\"pu_jit_geo.h\"", "-Wno-c99-designator",
+                                  "-Werror=missing-field-initializers"};
     if (waves_1level > 0) o.push_back("-DPU_WAVES_1LEVEL=" + std::to_string(waves_1level));
     return o;
 }
@@ -158,6 +165,7 @@ int compile(const std::string& geo_src, const std::vector<std::string>& opts, st
 }
 
 std::mutex g_jit_mu;   // one compile at a time per process (hipRTC holds a lot of memory)
+constexpr const char* kBuildArch = "gfx950";   // the library's own target (Makefile ARCH)
 
 }  // namespace
 
@@ -166,78 +174,134 @@ bool jit_enabled() {
     return !(e && e[0] == '0');
 }
 
-std::string jit_key(const Geo& g, int waves_1level) {
-    uint64_t h = fnv1a("primeuncore-jit-1");
+// The engine sources this library embeds, as 8 hex digits: the prefix of
+// every code object name it writes (tools/jit_warm.py keeps the code objects
+// whose prefix a library in the tree carries).
+std::string jit_source_tag() {
+    uint64_t h = fnv1a("primeuncore-jit-src");
+    for (int i = 0; i < pu_jit_nsrc; i++) {
+        h = fnv1a(pu_jit_src_name[i], h);
+        h = fnv1a(pu_jit_src_text[i], h);
+    }
+    char buf[9];
+    std::snprintf(buf, sizeof buf, "%08llx", (unsigned long long)(h >> 32));
+    return buf;
+}
+
+std::string jit_key(const Geo& g, int waves_1level, const std::string& arch) {
+    uint64_t h = fnv1a("primeuncore-jit-2");
     for (int i = 0; i < pu_jit_nsrc; i++) {
         h = fnv1a(pu_jit_src_name[i], h);
         h = fnv1a(pu_jit_src_text[i], h);
     }
     h = fnv1a(geo_cxx(g), h);
-    for (const auto& o : options(waves_1level)) h = fnv1a(o, h);
+    for (const auto& o : options(arch, waves_1level)) h = fnv1a(o, h);
     int maj = 0, min = 0;
     hiprtcVersion(&maj, &min);
     h = fnv1a(std::to_string(maj) + "." + std::to_string(min), h);
     char buf[17];
     std::snprintf(buf, sizeof buf, "%016llx", (unsigned long long)h);
-    return buf;
+    return jit_source_tag() + "-" + buf;
 }
+
+namespace {
+int jit_waves() {
+    const char* e = std::getenv("PRIMEUNCORE_JIT_WAVES");
+    return e && *e ? std::atoi(e) : 0;
+}
+
+// The current device's target ("gfx950" from "gfx950:sramecc+:xnack-").
+std::string device_arch() {
+    int dev = 0;
+    hipDeviceProp_t p;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return kBuildArch;
+    std::string a = p.gcnArchName;
+    const size_t k = a.find(':');
+    return a.empty() ? std::string(kBuildArch) : a.substr(0, k);
+}
+
+// Compile configuration g for arch into the cache; 0 or -1 (log filled).
+int compile_into(const Geo& g, int waves, const std::string& arch, const std::string& path,
+                 std::vector<char>* code, std::string* log) {
+    if (compile(geo_cxx(g), options(arch, waves), code, log) != 0) return -1;
+    ::mkdir(cache_dir().c_str(), 0755);
+    write_file_atomic(path, *code);
+    return 0;
+}
+
+// Load the kernels from a code object; false (module unloaded) on failure.
+bool load_module(const std::vector<char>& code, JitKernels* out, std::string* why) {
+    hipModule_t mod = nullptr;
+    if (hipModuleLoadData(&mod, code.data()) != hipSuccess) {
+        *why = "the device refused the code object";
+        return false;
+    }
+    static const char* names[3][2] = {{"pu_jit_uncore_s0_h0", "pu_jit_uncore_s0_h1"},
+                                      {"pu_jit_uncore_s1_h0", "pu_jit_uncore_s1_h1"},
+                                      {"pu_jit_uncore_s2_h0", nullptr}};
+    for (int s = 0; s < 3; s++)
+        for (int h = 0; h < 2; h++)
+            if (names[s][h] && hipModuleGetFunction(&out->f[s][h], mod, names[s][h]) != hipSuccess) {
+                (void)hipModuleUnload(mod);
+                *why = std::string("the code object lacks ") + names[s][h];
+                return false;
+            }
+    out->mod = mod;
+    return true;
+}
+}  // namespace
 
 int jit_load(const Geo& g, JitKernels* out, bool verbose) {
     *out = JitKernels{};
     if (!jit_enabled()) return 0;
-    int waves = 0;
-    if (const char* e = std::getenv("PRIMEUNCORE_JIT_WAVES"); e && *e) waves = std::atoi(e);
-    const std::string key = jit_key(g, waves);
-    const std::string dir = cache_dir();
-    const std::string path = dir + "/" + key + ".hsaco";
+    const int waves = jit_waves();
+    const std::string arch = device_arch();
+    const std::string key = jit_key(g, waves, arch);
+    const std::string path = cache_dir() + "/" + key + ".hsaco";
+    std::lock_guard<std::mutex> lk(g_jit_mu);   // one compile at a time; another thread may have built it
     std::vector<char> code;
-    bool cached = read_file(path, &code);
-    if (!cached) {
-        std::lock_guard<std::mutex> lk(g_jit_mu);
-        cached = read_file(path, &code);   // another thread of this process may have built it
-        if (!cached) {
-            std::string log;
-            if (verbose) std::fprintf(stderr, "[primeuncore] compiling the engine for this configuration (%s)\n", key.c_str());
-            if (compile(geo_cxx(g), options(waves), &code, &log) != 0) {
-                std::fprintf(stderr,
-                             "[primeuncore] compile-time configuration unavailable (hipRTC failed); the "
-                             "ahead-of-time kernels run instead:\n%s\n",
-                             log.c_str());
-                return 0;
-            }
-            ::mkdir(dir.c_str(), 0755);
-            write_file_atomic(path, code);
+    const bool cached = read_file(path, &code);
+    std::string log, why;
+    if (cached) {
+        ::utime(path.c_str(), nullptr);          // in use: tools/jit_warm.py keeps what is used
+        if (load_module(code, out, &why)) {
+            out->ok = true;
+            out->key = key;
+            return 0;
         }
+        // a damaged or foreign cache entry: drop it and compile once more
+        std::fprintf(stderr, "[primeuncore] cached code object %s: %s; compiling it again\n", path.c_str(),
+                     why.c_str());
+        std::remove(path.c_str());
+        *out = JitKernels{};
     }
-    hipModule_t mod = nullptr;
-    if (hipModuleLoadData(&mod, code.data()) != hipSuccess) {
-        std::fprintf(stderr, "[primeuncore] could not load the configuration's code object %s; ahead-of-time "
-                             "kernels run instead\n", path.c_str());
+    if (verbose) std::fprintf(stderr, "[primeuncore] compiling the engine for this configuration (%s)\n", key.c_str());
+    if (compile_into(g, waves, arch, path, &code, &log) != 0) {
+        std::fprintf(stderr,
+                     "[primeuncore] compile-time configuration unavailable (hipRTC failed); the ahead-of-time "
+                     "kernels run instead:\n%s\n",
+                     log.c_str());
         return 0;
     }
-    static const char* names[2][2] = {{"pu_jit_uncore_s0_h0", "pu_jit_uncore_s0_h1"},
-                                      {"pu_jit_uncore_s1_h0", "pu_jit_uncore_s1_h1"}};
-    for (int s = 0; s < 2; s++)
-        for (int h = 0; h < 2; h++)
-            if (hipModuleGetFunction(&out->f[s][h], mod, names[s][h]) != hipSuccess) {
-                (void)hipModuleUnload(mod);
-                *out = JitKernels{};
-                return set_error(PU_EIO, std::string("JIT code object lacks ") + names[s][h]);
-            }
-    out->mod = mod;
+    if (!load_module(code, out, &why)) {
+        std::fprintf(stderr, "[primeuncore] freshly compiled code object %s: %s; the ahead-of-time kernels run "
+                             "instead\n", path.c_str(), why.c_str());
+        std::remove(path.c_str());
+        *out = JitKernels{};
+        return 0;
+    }
     out->ok = true;
     out->key = key;
     return 0;
 }
 
-// Compile (or find in the cache) without loading: needs no GPU (build-time warm-up).
+// Compile (or find in the cache) without loading: needs no GPU (build-time
+// warm-up), so it targets the architecture the library is built for.
 int jit_warm(const Geo& g, std::string* key_out) {
-    int waves = 0;
-    if (const char* e = std::getenv("PRIMEUNCORE_JIT_WAVES"); e && *e) waves = std::atoi(e);
-    const std::string key = jit_key(g, waves);
+    const int waves = jit_waves();
+    const std::string key = jit_key(g, waves, kBuildArch);
     if (key_out) *key_out = key;
-    const std::string dir = cache_dir();
-    const std::string path = dir + "/" + key + ".hsaco";
+    const std::string path = cache_dir() + "/" + key + ".hsaco";
     struct stat st;
     if (::stat(path.c_str(), &st) == 0 && st.st_size > 0) {
         ::utime(path.c_str(), nullptr);   // still in use (tools/jit_warm.py prunes what is not)
@@ -245,9 +309,7 @@ int jit_warm(const Geo& g, std::string* key_out) {
     }
     std::vector<char> code;
     std::string log;
-    if (compile(geo_cxx(g), options(waves), &code, &log) != 0) return set_error(PU_EIO, "hipRTC: " + log);
-    ::mkdir(dir.c_str(), 0755);
-    write_file_atomic(path, code);
+    if (compile_into(g, waves, kBuildArch, path, &code, &log) != 0) return set_error(PU_EIO, "hipRTC: " + log);
     return 0;
 }
 
@@ -258,11 +320,12 @@ void jit_unload(JitKernels* k) {
 
 int jit_launch(const JitKernels& k, bool sliced, bool lds_headers, int nblocks, hipStream_t stream, const Geo* d_geo,
                char* arena, int replica0, const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
-               uint64_t budget_ticks, uint32_t flags) {
+               uint64_t budget_ticks, uint32_t flags, uint32_t* sched, int nrep) {
     void* args[] = {(void*)&d_geo, (void*)&arena, (void*)&replica0, (void*)&reqs, (void*)&off,
-                    (void*)&delays, (void*)&pos, (void*)&budget_ticks, (void*)&flags};
+                    (void*)&delays, (void*)&pos, (void*)&budget_ticks, (void*)&flags, (void*)&sched, (void*)&nrep};
     // latency mode (headers in LDS): two waves, the second the M/G/1 helper (engine.hip)
-    hipError_t e = hipModuleLaunchKernel(k.f[sliced ? 1 : 0][lds_headers ? 1 : 0], (unsigned)nblocks, 1, 1,
+    hipFunction_t f = sched ? k.f[2][0] : k.f[sliced ? 1 : 0][lds_headers ? 1 : 0];
+    hipError_t e = hipModuleLaunchKernel(f, (unsigned)nblocks, 1, 1,
                                          lds_headers ? 128 : 64, 1, 1, 0, stream, args, nullptr);
     return e == hipSuccess ? 0 : PU_EIO;
 }

@@ -10,17 +10,19 @@
 
 namespace pu {
 
-// The four launch shapes (time-sliced or not x queue headers in LDS or not)
-// of the engine compiled for one configuration.
+// The launch shapes of the engine compiled for one configuration: fixed
+// ranges / time-sliced / replica pool (f[0..2]) x queue headers in HBM or in
+// LDS (f[.][0..1]; the pool runs with headers in HBM only).
 struct JitKernels {
     hipModule_t mod = nullptr;
-    hipFunction_t f[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    hipFunction_t f[3][2] = {{nullptr, nullptr}, {nullptr, nullptr}, {nullptr, nullptr}};
     bool ok = false;
     std::string key;
 };
 
 bool jit_enabled();
-std::string jit_key(const Geo& g, int waves_1level);
+std::string jit_source_tag();
+std::string jit_key(const Geo& g, int waves_1level, const std::string& arch);
 // Load (compiling on a cache miss) the kernels of configuration g; leaves
 // out->ok false, after a message, when the specialisation is off or fails.
 int jit_load(const Geo& g, JitKernels* out, bool verbose);
@@ -29,7 +31,7 @@ int jit_warm(const Geo& g, std::string* key_out);
 void jit_unload(JitKernels* k);
 int jit_launch(const JitKernels& k, bool sliced, bool lds_headers, int nblocks, hipStream_t stream, const Geo* d_geo,
                char* arena, int replica0, const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
-               uint64_t budget_ticks, uint32_t flags);
+               uint64_t budget_ticks, uint32_t flags, uint32_t* sched = nullptr, int nrep = 0);
 int jit_occupancy(const JitKernels& k, int* blocks_per_cu);
 
 }  // namespace pu

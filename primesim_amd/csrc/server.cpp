@@ -132,7 +132,8 @@ struct Exec {
     // PU_ERRF_LIMITS bits of session s after the last run (0: exact so far)
     virtual uint64_t limit_flags(int) { return 0; }
     // index (into the last run's reqs) of the first request of session s that
-    // raised one of them: every request before it is exact.  0 = unknown.
+    // raised one of them: every request before it is exact.  0 = unknown;
+    // UINT64_MAX = none in the last run (the bits then predate it).
     virtual uint64_t limit_at(int) { return 0; }
 };
 
@@ -550,7 +551,12 @@ int serve_round(pu_server* s, int timeout_ms) {
             Session& S = s->sess[(size_t)b.session];
             if (S.ended) continue;
             const uint64_t lim = s->exec->limit_flags(b.session);
-            if (lim && off[(size_t)b.session] + b.first + b.n > s->exec->limit_at(b.session)) {
+            const uint64_t at = s->exec->limit_at(b.session);
+            // the limit bits are sticky across launches, the position is this
+            // launch's: a bit with no position here was raised before this
+            // launch (a handle stopped before serving, or served again after
+            // pu_server_stop), so every request of this launch is suspect
+            if (lim && (at == UINT64_MAX || off[(size_t)b.session] + b.first + b.n > at)) {
                 // an engine limit stopped the replica where the reference continues:
                 // batches that ended before the request that hit it were answered
                 // exactly above; no reply is exact from here on: end the session

@@ -35,7 +35,8 @@
 
 extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, int replica0, int nblocks,
                                 const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
-                                uint64_t budget_ticks, uint32_t flags, int lds_headers, hipStream_t stream);
+                                uint64_t budget_ticks, uint32_t flags, int lds_headers, uint32_t* sched, int nrep,
+                                hipStream_t stream);
 extern "C" int pu_engine_lds_header_queues(void);
 extern "C" int pu_engine_init_pool(char* arena, uint64_t replica_bytes, uint64_t off_pool_free, uint64_t off_run,
                                    int pool_entries, int nreplicas, hipStream_t stream);
@@ -398,14 +399,15 @@ int wait_stream(hipStream_t s) {
 
 int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
            hipStream_t s, uint64_t* d_pos = nullptr, uint64_t budget_ticks = 0, uint32_t extra_flags = 0,
-           bool short_launch = false, bool use_replay_mode = true) {
+           bool short_launch = false, bool use_replay_mode = true, uint32_t* d_sched = nullptr) {
     HIP_TRY(hipEventRecord(h->ev0, s), PU_EIO);
     // latency mode: with at most one replica per CU each wave keeps its queue
     // headers in the CU's LDS for the launch (engine.hip, LH). Copying the
     // image in and out costs ~17 us a launch, more than a short host batch
     // (a lone uncore_access, one MEM_REQUESTS message) wins back, so those
     // run with the headers in HBM (tools/latency_bench.py)
-    const int lh = h->lds_headers_ok && nblocks <= h->cus && !short_launch ? 1 : 0;
+    // (a replica-pool launch is always a throughput launch)
+    const int lh = h->lds_headers_ok && nblocks <= h->cus && !short_launch && !d_sched ? 1 : 0;
     const uint32_t flags = (extra_flags & PU_KF_NOHALT) || !use_replay_mode ? extra_flags
                                                                           : (h->replay_flags | extra_flags);
     // latency launches run the compiled configuration (one simulation alone +23%
@@ -414,9 +416,9 @@ int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const 
     // profiles/r3o_ab_opq.txt) unless PRIMEUNCORE_JIT_THROUGHPUT=0
     const bool use_jit = h->jit.ok && (lh != 0 || h->jit_throughput);
     int rc = use_jit ? pu::jit_launch(h->jit, d_pos != nullptr, lh != 0, nblocks, s, h->d_geo, h->arena, replica0,
-                                        d_reqs, d_off, d_delay, d_pos, budget_ticks, flags)
+                                        d_reqs, d_off, d_delay, d_pos, budget_ticks, flags, d_sched, h->R)
                        : pu_engine_launch(h->d_geo, h->geo.num_levels, h->arena, replica0, nblocks, d_reqs, d_off,
-                                          d_delay, d_pos, budget_ticks, flags, lh, s);
+                                          d_delay, d_pos, budget_ticks, flags, lh, d_sched, h->R, s);
     if (rc) return pu::set_error(rc, "engine launch failed");
     HIP_TRY(hipEventRecord(h->ev1, s), PU_EIO);
     return 0;
@@ -531,6 +533,11 @@ int pu_config_jit_warm(const pu_sim_cfg* cfg) {
 }
 
 int pu_compiled_config(const pu_handle* h) { return h && h->jit.ok ? (h->jit_throughput ? 2 : 1) : 0; }
+
+const char* pu_jit_source_tag(void) {
+    static const std::string tag = pu::jit_source_tag();
+    return tag.c_str();
+}
 
 long pu_config_geo_source(const pu_sim_cfg* cfg, char* buf, size_t cap) {
     if (!cfg) return pu::set_error(PU_EINVAL, "bad arguments");
@@ -844,6 +851,28 @@ int pu_run_device_sliced(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_o
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
     std::lock_guard<std::mutex> lk(h->mu);
     return launch(h, 0, h->R, d_reqs, d_off, d_delay, s, d_pos, budget_us * 100);   // s_memrealtime: 100 MHz
+}
+
+int pu_pool_slots(pu_handle* h) {
+    if (!h) return pu::set_error(PU_EINVAL, "null handle");
+    const int res = pu_resident_replicas(h);
+    if (res < 0) return res;
+    return res < h->R ? res : h->R;
+}
+
+long pu_pool_words(int slots) { return slots < 1 ? pu::set_error(PU_EINVAL, "slots < 1") : (long)PU_POOL_WORDS(slots); }
+
+int pu_run_device_pool(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
+                       uint64_t* d_pos, uint32_t* d_sched, int slots, uint64_t budget_us, void* hip_stream) {
+    if (!h || !d_reqs || !d_off || !d_delay || !d_pos || !d_sched || budget_us == 0)
+        return pu::set_error(PU_EINVAL, "bad arguments (the pool needs a time slice: budget_us > 0)");
+    const int most = pu_pool_slots(h);
+    if (most < 0) return most;
+    if (slots < 1 || slots > most)
+        return pu::set_error(PU_ERANGE, "slots must be 1.." + std::to_string(most) + " (pu_pool_slots)");
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    std::lock_guard<std::mutex> lk(h->mu);
+    return launch(h, 0, slots, d_reqs, d_off, d_delay, s, d_pos, budget_us * 100, 0, false, true, d_sched);
 }
 
 int pu_synchronize(pu_handle* h) {

@@ -58,6 +58,7 @@ def lib() -> C.CDLL:
         "pu_config_geo_source": (C.c_long, [P(A.SimCfg), C.c_char_p, C.c_size_t]),
         "pu_config_jit_warm": (C.c_int, [P(A.SimCfg)]),
         "pu_compiled_config": (C.c_int, [C.c_void_p]),
+        "pu_jit_source_tag": (C.c_char_p, []),
         "pu_destroy": (None, [C.c_void_p]),
         "pu_reset": (C.c_int, [C.c_void_p]),
         "pu_num_replicas": (C.c_int, [C.c_void_p]),
@@ -75,6 +76,10 @@ def lib() -> C.CDLL:
         "pu_run_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
         "pu_run_device_sliced": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                            C.c_void_p]),
+        "pu_pool_slots": (C.c_int, [C.c_void_p]),
+        "pu_pool_words": (C.c_long, [C.c_int]),
+        "pu_run_device_pool": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_int, C.c_uint64, C.c_void_p]),
         "pu_synchronize": (C.c_int, [C.c_void_p]),
         "pu_core_completion": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
         "pu_stats_get": (C.c_int, [C.c_void_p, C.c_int, P(A.Stats)]),
@@ -468,6 +473,31 @@ class UncoreManager:
                                         stream_ptr or None)
         if rc != 0:
             raise UncoreError(f"run_device_sliced: {last_error()}")
+
+    def pool_slots(self) -> int:
+        """Most wavefronts of a replica-pool launch: min(replicas, resident replicas)."""
+        n = lib().pu_pool_slots(self._handle())
+        if n < 0:
+            raise UncoreError(f"pool_slots: {last_error()}")
+        return int(n)
+
+    @staticmethod
+    def pool_words(slots: int) -> int:
+        """uint32 words of the scheduling array a pool of `slots` wavefronts needs (all 0 to start)."""
+        n = lib().pu_pool_words(slots)
+        if n < 0:
+            raise UncoreError(f"pool_words: {last_error()}")
+        return int(n)
+
+    def run_device_pool(self, d_reqs_ptr: int, d_off_ptr: int, d_delay_ptr: int, d_pos_ptr: int, d_sched_ptr: int,
+                        slots: int, budget_us: int, stream_ptr: int = 0) -> None:
+        """Time-sliced run of more replicas than run at once: each of `slots`
+        wavefronts continues its replica and, once that replica's range is done
+        (or it halted), takes the next unstarted one (pu_run_device_pool)."""
+        rc = lib().pu_run_device_pool(self._handle(), d_reqs_ptr, d_off_ptr, d_delay_ptr, d_pos_ptr, d_sched_ptr,
+                                      slots, budget_us, stream_ptr or None)
+        if rc != 0:
+            raise UncoreError(f"run_device_pool: {last_error()}")
 
     def synchronize(self) -> None:
         if lib().pu_synchronize(self._handle()) != 0:

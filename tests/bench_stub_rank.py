@@ -34,9 +34,10 @@ class StubDevice:
     def __init__(self, args, cfg, threads, rank, local):
         self.cfg, self.threads = cfg, threads
         self.R, self.um, self.dev, self.stream = REPLICAS, StubUM(), None, None
+        self.slots = REPLICAS
         self.compiled = 0
 
-    def headline(self, args, rank, world):
+    def headline(self, args, rank, world, keep):
         import oracle as O
         import primesim_amd as P
         from primesim_amd.dist import replica_seed
@@ -57,8 +58,8 @@ class StubDevice:
         with open(os.path.join(os.environ["PU_STUB_OUT"], f"rank{rank}.txt"), "w") as f:
             f.write(f"{processed} {int(sum(int(x.astype(np.int64).sum()) for x in rep0))}\n")
         return bench.Pass(elapsed=0.5 + rank, kern_ms=[1.0] * args.steps, adv=np.array([REQS_PER_REPLICA] * self.R),
-                          rep0=rep0, delta=delta, halted=0, errf=0, per_replica=None, steps=args.steps,
-                          processed=processed)
+                          kept={0: rep0[0]}, delta=delta, halted=0, errf=0, per_replica=None, steps=args.steps,
+                          processed=processed, pool=None)
 
     def reduce_device(self, args):
         return None

@@ -26,3 +26,34 @@ def test_cpu_baseline_stops_at_the_halt():
     stop = int(nz[-1]) + 1                       # the golden: delays are 0 after the stopping request
     assert n_sim == stop < len(c.reqs)
     np.testing.assert_array_equal(d[:stop], c.delays[:stop])
+
+
+def test_parity_replicas_spread_to_the_last():
+    reps = bench.parity_replicas(5120, 16)
+    assert len(reps) == 16 and reps[0] == 0 and reps[-1] == 5119
+    assert reps == sorted(set(reps)) and reps[1] == 320
+    assert bench.parity_replicas(10, 16) == list(range(10))
+    assert bench.parity_replicas(1, 16) == [0]
+
+
+def test_ensemble_returns_the_delays_of_its_replicas(tmp_path):
+    """The ensemble processes (forked before the GPU is touched) are told their
+    replicas afterwards and send back every delay they produced: the same
+    delays the CPU restatement gives on those replicas' streams."""
+    import oracle as O
+    from primesim_amd import config as CF
+    from primesim_amd.dist import replica_seed
+    xml = CF.write_xml(CF.preset("C4"), str(tmp_path / "c4.xml"))
+    ens = bench.Ensemble(xml, 3, 3000, 3000, 0.3)
+    assert ens.assign(40) == [0, 13, 39]
+    res = ens.run()
+    assert res["cores"] == 3 and sorted(ens.delays) == [0, 13, 39]
+    cfg = P.load_config(xml)
+    for r, got in ens.delays.items():
+        assert len(got) >= 3000
+        reqs = P.generate_stream(bench.stream_spec(replica_seed(bench.SEED_BASE, 0, r), len(got)))
+        ref = O.CpuRef(cfg)
+        for prog, th in P.stream_threads(bench.stream_spec(bench.SEED_BASE)):
+            ref.alloc_core(prog, th)
+        want, _ = ref.run(reqs)
+        np.testing.assert_array_equal(got, want[:len(got)])

@@ -249,3 +249,42 @@ def test_engine_limit_mid_round_answers_the_batches_before_it(monkeypatch, tmp_p
     finally:
         srv.close()
         um.close()
+
+
+def test_served_handle_already_stopped_by_an_engine_limit(monkeypatch, tmp_path):
+    """A handle whose replica hit an engine limit before serving started (the
+    server never resets it): the replica is halted, so the engine writes 0 for
+    every request of every later launch.  The limit bit is sticky but the
+    limit position belongs to the earlier launch, so the server sees a limit
+    with no position in this launch: it must end the session as failed
+    instead of answering those zeros."""
+    c = Case("c4_allcores")
+    cfg = P.load_config(c.xml_path)
+    monkeypatch.setenv("PRIMEUNCORE_POOL_ENTRIES", "2")
+    um = P.UncoreManager()
+    um.init(cfg, replicas=1)
+    monkeypatch.delenv("PRIMEUNCORE_POOL_ENTRIES")
+    for prog, th in c.threads:
+        um.allocCore(prog, th)
+    with pytest.raises(UncoreError):
+        um.access_batch(c.reqs)                                     # the pool runs out
+    assert int(um.limit_positions(1)[0]) < len(c.reqs)
+    path = _sock()
+    srv = S.PrimeServer(um, path)
+    try:
+        srv.start()
+        drv = S.CoreManagerDriver(path, 0, c.threads)
+        drv.start()
+        starts = np.nonzero(c.reqs["batch_start"])[0].tolist() + [len(c.reqs)]
+        b = c.reqs[starts[0]:starts[1]]
+        p, t = c.threads[int(b[0]["core"])]
+        drv.clients[p].send(S.mem_message(t, b), tag=drv.tag_of[(p, t)])
+        with pytest.raises(UncoreError):
+            drv.clients[p].recv(t)                                  # EOF: no exact reply exists
+        assert srv.join(30) == 0
+        st = srv.stats()
+        assert st["sessions_failed"] == 1 and st["sessions_ended"] == 1
+        drv.close()
+    finally:
+        srv.close()
+        um.close()

@@ -1,0 +1,80 @@
+#!/bin/bash
+# One GPU-box session: run the named steps in order, each under its own time
+# limit, stopping at the first failure (no step is retried).  Outputs go to
+# gpurun_out/TAG_*.  Replaces round 3's one-off tools/r3_*.sh scripts.
+#
+#   tools/gpu_session.sh TAG STEP [STEP ...]
+#
+# Steps:
+#   tests        pytest -m gpu (the whole GPU parity suite)
+#   smoke        __graft_entry__.smoke()
+#   traffic      PMC fabric traffic of the headline kernel on the driver's window (tools/pmc_traffic.py)
+#   bench        bench.py on the driver's config (--steps 20 --warmup 5), carrying TAG_traffic.json if present
+#   bench_default  bench.py with no flags
+#   rocprof      rocprofv3 --kernel-trace --stats of the driver's config (headline only)
+#   sq           SQ wave-state / instruction counters of the headline kernel (tools/pmc_sq.py)
+#   sq_single    the same for one simulation alone, open loop and closed loop (latency kernel)
+#   handoff      tools/probe/handoff: dependent hand-off latency between two waves
+#   tworank      bench.py --gpus 2 with both ranks on card 0 (gloo)
+#   regions_single  lone-wave region profiles (PU_PROF build, libprimeuncore_prof.so), open and closed loop
+#   ab_modes:V1,V2,...   interleaved same-box A/B of engine libraries (main = libprimeuncore.so, else
+#                libprimeuncore_V.so) in three regimes: headline, one simulation alone open / closed loop
+#   ab_single:V1,V2,...  the same, one simulation alone only
+#   ab_ens:V1,V2,...     the same, headline only (3 rounds)
+#   ab_pool      headline with the replica pool (--spare-replicas 0.1) vs without (0), 3 interleaved rounds
+set -o pipefail
+T=$1; shift
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+O=gpurun_out/${T}
+BENCH="python bench.py"
+DRIVER="--steps 20 --warmup 5"
+
+ab() {   # ab ROUNDS MODES VARIANTS
+  local R=$1 MODES=$2 VARS=$3 mode v ARGS
+  for i in $(seq 1 "$R"); do
+    for mode in $MODES; do
+      case $mode in
+        ens) ARGS="--steps 5 --warmup 5 --no-cpu --no-extras";;
+        single) ARGS="--replicas 1 --steps 3 --warmup 5 --no-cpu --no-extras";;
+        closed) ARGS="--replicas 1 --steps 3 --warmup 5 --no-cpu --no-extras --replay closed";;
+      esac
+      for v in ${VARS//,/ }; do
+        ( if [ "$v" != main ]; then export PRIMEUNCORE_LIB=$PWD/primesim_amd/libprimeuncore_$v.so; fi
+          timeout -k 10 200 $BENCH $ARGS 2>>${O}_ab.err | python -c "import json,sys; b=json.loads(sys.stdin.read().strip().splitlines()[-1]); v=b['value']; print('$mode', '$v', round(v) if v < 1e6 else round(v / 1e6, 2), flush=True)" ) || return 1
+      done
+    done
+  done
+}
+
+for S in "$@"; do
+  echo "[gpu_session] $T: $S ($(date +%T))"
+  case $S in
+    tests) timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > ${O}_gpu_tests.log 2>&1 || exit 1;;
+    smoke) timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > ${O}_smoke.log 2>&1 || exit 1;;
+    traffic) timeout -k 10 500 python tools/pmc_traffic.py --work /tmp/pmc --out ${O}_traffic.json -- $DRIVER --no-cpu --no-extras > ${O}_traffic.log 2>&1 || exit 1;;
+    bench) TJ=""; [ -f ${O}_traffic.json ] && TJ="--traffic-json ${O}_traffic.json"
+           timeout -k 10 400 $BENCH $DRIVER $TJ > ${O}_bench.json 2> ${O}_bench.log || exit 1;;
+    bench_default) timeout -k 10 400 $BENCH > ${O}_bench_default.json 2> ${O}_bench_default.log || exit 1;;
+    rocprof) TJ=""; [ -f ${O}_traffic.json ] && TJ="--traffic-json ${O}_traffic.json"
+             timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/${T}_prof -o run -- python3 bench.py $DRIVER --no-cpu --no-extras $TJ > ${O}_bench_under_rocprof.json 2> ${O}_rocprof.log || exit 1
+             cp /tmp/${T}_prof/run_kernel_stats.csv ${O}_kernel_stats.csv || exit 1;;
+    sq) timeout -k 10 700 python tools/pmc_sq.py --work /tmp/pmc_sq --out ${O}_sq.json -- --steps 3 --warmup 5 --no-cpu --no-extras > ${O}_sq.log 2>&1 || exit 1;;
+    sq_single) timeout -k 10 500 python tools/pmc_sq.py --kernel pu_jit_uncore_s1_h1 --work /tmp/pmc_sq1 --out ${O}_sq_single_open.json -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras > ${O}_sq_single_open.log 2>&1 || exit 1
+               timeout -k 10 500 python tools/pmc_sq.py --kernel pu_jit_uncore_s1_h1 --work /tmp/pmc_sq2 --out ${O}_sq_single_closed.json -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras --replay closed > ${O}_sq_single_closed.log 2>&1 || exit 1;;
+    handoff) timeout -k 10 120 tools/probe/handoff > ${O}_handoff.json 2> ${O}_handoff.log || exit 1;;
+    tworank) PU_BENCH_DEVICE=0 timeout -k 10 300 $BENCH --gpus 2 --steps 3 --warmup 2 --no-cpu --dist-backend gloo > ${O}_two_rank.json 2> ${O}_two_rank.log || exit 1;;
+    regions_single)
+      PROF_LIB=$PWD/primesim_amd/libprimeuncore_prof.so timeout -k 10 200 python tools/prof_regions.py -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras > ${O}_regions_single_open.txt 2>&1 || exit 1
+      PROF_LIB=$PWD/primesim_amd/libprimeuncore_prof.so timeout -k 10 200 python tools/prof_regions.py -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras --replay closed > ${O}_regions_single_closed.txt 2>&1 || exit 1;;
+    ab_modes:*) ab 2 "ens single closed" "${S#ab_modes:}" > ${O}_ab_modes.txt || exit 1;;
+    ab_single:*) ab 2 "single closed" "${S#ab_single:}" > ${O}_ab_single.txt || exit 1;;
+    ab_ens:*) ab 3 "ens" "${S#ab_ens:}" > ${O}_ab_ens.txt || exit 1;;
+    ab_pool) for i in 1 2 3; do for sp in 0.1 0; do
+               timeout -k 10 300 $BENCH $DRIVER --no-cpu --no-extras --spare-replicas $sp 2>>${O}_ab.err | python -c "import json,sys; b=json.loads(sys.stdin.read().strip().splitlines()[-1]); c=b['config']; p=c.get('replica_pool') or {}; print('spare $sp', round(b['value']/1e6,2), 'M/s', 'replicas', c['replicas_per_gpu'], 'halted', c['halted_replicas'], 'busy', round(p.get('busy_fraction', 0), 4), flush=True)" >> ${O}_ab_pool.txt || exit 1
+             done; done;;
+    *) echo "unknown step $S"; exit 2;;
+  esac
+done
+du -sh gpurun_out
+exit 0

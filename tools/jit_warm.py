@@ -1,6 +1,6 @@
 """Warm the compile-time-configuration cache (primesim_amd/jit_cache/) for every
 configuration the GPU tests, smoke() and bench.py use: the golden XMLs, the
-C1-C5 presets and the DRAM-bank test geometries.  Runs on the CPU (hipRTC needs
+C1-C5 presets, the DRAM-bank test geometries and tests/extra_configs.py.  Runs on the CPU (hipRTC needs
 no GPU), several compiles at once; a configuration already cached is skipped.
 
     python3 tools/jit_warm.py [-j N]
@@ -11,11 +11,13 @@ import argparse
 import ctypes as C
 import glob
 import os
+import subprocess
 import sys
 import time
 from concurrent.futures import ProcessPoolExecutor
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PRUNE_HOURS = 1   # grace for code objects written by a library being rebuilt
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
@@ -33,7 +35,26 @@ def configs():
         out.extend(dram_configs())
     except ImportError:
         pass
+    try:
+        from extra_configs import extra_configs
+        out.extend(extra_configs())
+    except ImportError:
+        pass
     return out
+
+
+def live_source_tags() -> set:
+    """Source tags (pu_jit_source_tag) of every engine library in the tree:
+    the product library and experiment builds (libprimeuncore_*.so).  Each is
+    asked in a child process, so their identical symbol names never meet."""
+    tags = set()
+    for lib in glob.glob(os.path.join(ROOT, "primesim_amd", "libprimeuncore*.so")):
+        r = subprocess.run([sys.executable, "-c", "import ctypes, sys; f = ctypes.CDLL(sys.argv[1]).pu_jit_source_tag; "
+                            "f.restype = ctypes.c_char_p; print(f().decode())", lib],
+                           capture_output=True, text=True, timeout=60)
+        if r.returncode == 0 and r.stdout.strip():
+            tags.add(r.stdout.strip())
+    return tags
 
 
 def _warm(item):
@@ -61,14 +82,24 @@ def main() -> int:
                 print(f"[jit_warm] {name}: FAILED {err[:2000]}", flush=True)
             elif rc == 0:
                 print(f"[jit_warm] {name}: compiled in {dt:.1f}s", flush=True)
-    # drop code objects no current configuration uses (older sources or geometries)
-    cache = os.environ.get("PRIMEUNCORE_JIT_CACHE") or os.path.join(ROOT, "primesim_amd", "jit_cache")
-    stale = [f for f in glob.glob(os.path.join(cache, "*.hsaco")) if os.path.getmtime(f) < t0 - 1]
-    if not bad:
+    # drop code objects of the in-tree cache compiled from sources no library in
+    # the tree embeds (their name's prefix is the source tag), after an hour's
+    # grace: code objects pu_create compiled on demand for user configurations
+    # and those of experiment builds stay; a cache outside the tree
+    # (PRIMEUNCORE_JIT_CACHE) is never pruned
+    intree = os.path.join(ROOT, "primesim_amd", "jit_cache")
+    cache = os.environ.get("PRIMEUNCORE_JIT_CACHE") or intree
+    stale = []
+    if not bad and os.path.realpath(cache) == os.path.realpath(intree):
+        live = live_source_tags()
+        for f in glob.glob(os.path.join(cache, "*.hsaco")):
+            tag = os.path.basename(f).split("-")[0]
+            if tag not in live and os.path.getmtime(f) < t0 - PRUNE_HOURS * 3600:
+                stale.append(f)
         for f in stale:
             os.remove(f)
-    print(f"[jit_warm] {len(items)} configurations, {bad} failed, {len(stale) if not bad else 0} stale code objects "
-          f"removed, {time.time() - t0:.0f}s", flush=True)
+    print(f"[jit_warm] {len(items)} configurations, {bad} failed, {len(stale)} code objects of sources no library "
+          f"here compiles removed, {time.time() - t0:.0f}s", flush=True)
     return 1 if bad else 0
 
 

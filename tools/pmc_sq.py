@@ -20,9 +20,9 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# the timed (throughput) launches of bench.py: the ahead-of-time kernel, or the
-# compiled configuration's under PRIMEUNCORE_JIT_THROUGHPUT=1
-KERNEL = "uncore_kernel<1, true, false>|pu_jit_uncore_s1_h0"
+# the timed (throughput) launches of bench.py: time-sliced or replica-pool, the
+# compiled configuration's kernel or the ahead-of-time one
+KERNEL = "uncore_kernel<1, 1, false>|uncore_kernel<1, 2, false>|pu_jit_uncore_s1_h0|pu_jit_uncore_s2_h0"
 PASSES = [
     ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"],
     ["SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_LDS", "SQ_INSTS_VALU",
