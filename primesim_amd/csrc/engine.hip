@@ -2214,8 +2214,6 @@ __device__ __forceinline__ void stats_init() {
 
 // A replica-pool wave's own state (uncore_body), in LDS: lane 0 writes it.
 struct PoolCtl {
-    uint32_t* sched;
-    char* arena;
     int32_t nrep;
     int32_t r;            // the replica the wave holds, -1 = none
 };
@@ -2223,10 +2221,10 @@ static __shared__ PoolCtl lds_pool;
 // The replica a pool wave runs next: `cur` if it holds one, else the next
 // unstarted replica (sched[0], one device-scope atomic by lane 0); -1 once
 // every replica has been taken.
-__device__ __forceinline__ int pool_next(int cur) {
+__device__ __forceinline__ int pool_next(uint32_t* sched, int cur) {
     if (cur >= 0) return cur;
     uint32_t t = 0;
-    if (lane_id() == 0) t = __hip_atomic_fetch_add(&lds_pool.sched[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane_id() == 0) t = __hip_atomic_fetch_add(&sched[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int r = (int)rl32(t, 0);
     return r < (int)uni32((uint32_t)lds_pool.nrep) ? r : -1;
 }
@@ -2404,17 +2402,17 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
     int r = replica0 + (int)blockIdx.x;
     if constexpr (pool) {
         if (e.ln == 0) {
-            lds_pool.sched = sched;
-            lds_pool.arena = arena;
             lds_pool.nrep = nrep;
             lds_pool.r = (int32_t)sched[PU_POOL_SLOT0 + blockIdx.x] - 1;
         }
         __builtin_amdgcn_wave_barrier();
-        r = pool_next((int)uni32((uint32_t)lds_pool.r));
+        r = pool_next(sched, (int)uni32((uint32_t)lds_pool.r));
     }
     while (r >= 0) {
         if (pool && e.ln == 0) lds_pool.r = r;
-        e.base = (char*)uni64((uint64_t)(pool ? lds_pool.arena : arena)) + (size_t)r * OFF(e.g->replica_bytes);
+        // (pointer arithmetic on the kernel argument: the compiler keeps it a
+        // global-memory pointer, so the engine's accesses stay global_*, not flat_*)
+        e.base = arena + (size_t)r * OFF(e.g->replica_bytes);
         if constexpr (LH) {
             // Latency mode: a two-wave workgroup.  Both waves copy the replica's
             // queue headers into the LDS image (pieces a, b, c; d = no cached
@@ -2467,11 +2465,11 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
         if (!pool) break;
         // a pool wave: keep the replica if the slice ran out, else take the next
         if (!done) break;
-        r = pool_next(-1);
+        r = pool_next(sched, -1);
         if (r < 0 && e.ln == 0) lds_pool.r = -1;
     }
     if (pool && e.ln == 0) {
-        uint32_t* S = lds_pool.sched;
+        uint32_t* S = sched;
         S[PU_POOL_SLOT0 + blockIdx.x] = (uint32_t)(lds_pool.r + 1);
         S[PU_POOL_SLOT0 + gridDim.x + blockIdx.x] += (uint32_t)(__builtin_amdgcn_s_memrealtime() - wave_t0);
     }
