@@ -264,10 +264,8 @@ def test_served_handle_already_stopped_by_an_engine_limit(monkeypatch, tmp_path)
     um = P.UncoreManager()
     um.init(cfg, replicas=1)
     monkeypatch.delenv("PRIMEUNCORE_POOL_ENTRIES")
-    for prog, th in c.threads:
-        um.allocCore(prog, th)
-    with pytest.raises(UncoreError):
-        um.access_batch(c.reqs)                                     # the pool runs out
+    with pytest.raises(UncoreError):                                # (core ids come resolved in the
+        um.access_batch(c.reqs)                                     # requests): the pool runs out
     assert int(um.limit_positions(1)[0]) < len(c.reqs)
     path = _sock()
     srv = S.PrimeServer(um, path)
