@@ -600,6 +600,19 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
     return d;
 }
 
+// ---- SGPR lane-mask helpers (the latency kernel's window loop) ---------------
+// lane bit of m set ? b : a: one v_cndmask with the mask as its SGPR selector
+// (a predicate held as a wave mask never goes through a VGPR boolean)
+__device__ __forceinline__ uint32_t selm32(uint64_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    m = uni64(m);   // wave-uniform; a mask the compiler knows as a constant still goes in an SGPR pair
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+__device__ __forceinline__ uint64_t selm64(uint64_t m, uint64_t a, uint64_t b) {
+    const uint32_t lo = selm32(m, (uint32_t)a, (uint32_t)b), hi = selm32(m, (uint32_t)(a >> 32), (uint32_t)(b >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
 // Latency mode (LH): a launch with at most one replica per CU keeps every
 // queue header of its replica in the CU's LDS for the whole launch (copied in
 // at the start, back at the end), so the header round trip of each route
@@ -979,6 +992,80 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
             A0 = t + c.router + (S - e);
         }
         int js = 0;
+        if constexpr (LH) {
+            // latency kernel: the window's live hops and the M/G/1 hops'
+            // finish times as wave masks (one v_cndmask per dword), the
+            // staging slots as wrapping counters and a three-way DMA wait
+            // instead of a modulo and an eight-way ladder: one simulation
+            // alone +1.6% open loop, +3.4% closed loop (same-box A/B,
+            // profiles/r4d_ab_single.txt; a tree operation on wave masks,
+            // tree_op's predicates combined on the scalar unit, ran 9% slower
+            // closed loop: more scalar instructions than it saved)
+            const uint64_t nhm = nh >= 64 ? ~0ull : ((1ull << nh) - 1);
+            int islot = issued % PU_RING_PF, cslot = 0;
+            while (js < nh) {
+                const uint64_t live = nhm & (~0ull << js);
+                const uint64_t A = A0 + sh;
+                const uint64_t cand = ballot(vfront <= A + (uint64_t)plen) & live;
+                const int jt = cand ? (int)__builtin_ctzll(cand) : nh;
+                // hops [js, jt) took M/G/1: their finish times
+                const uint64_t fm = jt >= 64 ? live : live & ((1ull << jt) - 1);
+                vfin = selm64(fm, vfin, A + vd + (uint64_t)plen);
+                mg1 += (uint64_t)(jt - js);
+                if (jt == nh) {                               // the rest of the window is M/G/1
+                    t = t0 + rl64(S, nh - 1) + sh;
+                    break;
+                }
+                PROF_T(p_tree);
+                PROF_CNT(PF_TREEHOPS, 1);
+                const uint64_t tj = rl64(A, jt);
+                const int q = (int)rl32((uint32_t)rq, jt);
+                uint32_t head = rl32(vhead, jt), cnt = rl32(vcnt, jt);
+                uint64_t f0n, f1n, d;
+                RingView v;
+                const bool staged = mc && jt == (int)__builtin_ctzll(mc);
+                if (staged) {
+                    // predicted: its ring is (being) staged in LDS slot cslot
+                    mc &= mc - 1;
+                    PROF_T(p_wait);
+                    const int newer = issued - consumed - 1;  // rings issued after this one, < PU_RING_PF
+                    if (newer <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    else if (newer == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                    PROF_ADD(PF_NWAIT, p_wait);
+                    ring_from_lds(cslot, v);
+                    cslot = cslot == PU_RING_PF - 1 ? 0 : cslot + 1;
+                    consumed++;
+                } else {                            // not predicted (arrival pushed past the front)
+                    PROF_CNT(PF_DEMAND, 1);
+                    ring_load(c, q, head, cnt, v);
+                }
+                d = tree_op(c, q, v, head, cnt, tj, (uint64_t)plen, c.link_delay, err, f0n, f1n);
+                if (cnt >= PU_QMAX) {               // the next call's prune (history_tree.cpp:49-55), done now
+                    head = (head + 1) & (PU_QRING - 1);
+                    cnt--;
+                    f0n = f1n;
+                }
+                if (staged && mi) {                 // keep PF rings in flight
+                    PROF_T(p_r);
+                    const int jj = (int)__builtin_ctzll(mi);
+                    mi &= mi - 1;
+                    ring_dma(c, (int)rl32((uint32_t)rq, jj), rl32(vhead, jj), rl32(vcnt, jj), islot);
+                    islot = islot == PU_RING_PF - 1 ? 0 : islot + 1;
+                    issued++;
+                    PROF_ADD(PF_T_REFILL, p_r);
+                }
+                sh += d - rl64(vd, jt);
+                vhead = wl32(vhead, head, jt);
+                vcnt = wl32(vcnt, cnt, jt);
+                vf0 = wl64(vf0, f0n, jt);
+                vd = wl64(vd, d, jt);
+                vfin = wl64(vfin, tj + d + (uint64_t)plen, jt);
+                t = tj + d + c.link_delay;
+                js = jt + 1;
+                PROF_ADD(PF_NTREE, p_tree);
+            }
+        } else {
         while (js < nh) {
             const bool live = ln >= js && ln < nh;
             uint64_t A;
@@ -1042,6 +1129,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
             t = tj + d + c.link_delay;
             js = jt + 1;
             PROF_ADD(PF_NTREE, p_tree);
+        }
         }
         PROF_ADD(PF_NHOPS, p_hops);
         PROF_T(p_wb);
