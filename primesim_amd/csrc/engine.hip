@@ -1250,6 +1250,15 @@ struct Engine {
 
     template <class T>
     __device__ __forceinline__ T* at(uint64_t off) const {
+        if constexpr (LH) {
+            // latency kernel: the replica base made opaque at every use, so
+            // the compiler derives each region pointer where it is used
+            // instead of hoisting dozens of them out of the request loop
+            // (their SGPR pairs were spilled to VGPR lanes and reloaded)
+            AS1 char* b = (AS1 char*)base;
+            asm("" : "+s"(b));
+            return reinterpret_cast<T*>((char*)(b + off));
+        }
         return reinterpret_cast<T*>(base + off);
     }
 
@@ -1435,14 +1444,14 @@ struct Engine {
     // ------------------------------------------------------------ downward propagation
     // System::share / System::inval (system.cpp:488-555); LV is the level of `cid`.
     template <int LV, bool INVAL>
-    __device__ int down(int cid, const Req& r) {
+    __device__ __forceinline__ int down(int cid, const Req& r) {
         PROF_T(p0);
         int d = down_impl<LV, INVAL>(cid, r);
         PROF_ADD(PF_DOWN, p0);
         return d;
     }
     template <int LV, bool INVAL>
-    __device__ int down_impl(int cid, const Req& r) {
+    __device__ __forceinline__ int down_impl(int cid, const Req& r) {
         const LevelGeo& L = g->lv[LV];
         uint32_t alive_v = ln == (cid & 63) ? at<uint32_t>(OFF(L.off_alive))[cid] : 0u;
         SetView v;
@@ -1463,7 +1472,7 @@ struct Engine {
     }
     // share_children / inval_children (system.cpp:514-572): max over children.
     template <int LV, bool INVAL>
-    __device__ int children(int cid, const Req& r) {
+    __device__ __forceinline__ int children(int cid, const Req& r) {
         if constexpr (LV == 0) {
             return 0;
         } else {
@@ -1530,7 +1539,7 @@ struct Engine {
         *idx = rl32(v, 0);
         return true;
     }
-    __device__ int first_sharer(uint32_t nsh, uint64_t sh) {
+    __device__ __forceinline__ int first_sharer(uint32_t nsh, uint64_t sh) {
         if (nsh == PU_SH_POOL) {
             for (int base = 0; base < g->dir.nwords; base += 64) {
                 uint64_t w = pool_word(sh, base);
@@ -1546,7 +1555,7 @@ struct Engine {
         err_or(PU_ERRF_EMPTY_SHARER);     // *sharer_set.begin() on an empty set
         return 0;
     }
-    __device__ int count_sharers(uint32_t nsh, uint64_t sh) const {
+    __device__ __forceinline__ int count_sharers(uint32_t nsh, uint64_t sh) const {
         if (nsh != PU_SH_POOL) return (int)nsh;
         int c = 0;
         for (int base = 0; base < g->dir.nwords; base += 64) c += __builtin_popcountll(pool_word(sh, base));
@@ -1554,7 +1563,7 @@ struct Engine {
         return (int)uni32((uint32_t)c);
     }
     // sharer_set.insert(cid)
-    __device__ void add_sharer(uint32_t& nsh, uint64_t& sh, int cid) {
+    __device__ __forceinline__ void add_sharer(uint32_t& nsh, uint64_t& sh, int cid) {
         if (nsh == PU_SH_POOL) {
             if (ln == ((cid >> 6) & 63)) {
                 uint64_t* P = pool_of(sh) + (cid >> 6);
@@ -1605,7 +1614,7 @@ struct Engine {
     // into `delay` directly (delay += ...; timer + delay), a sharer set adds
     // the max over targets (initialised to 0) of times relative to
     // timer + delay: the two differ once an int wraps, so both are kept.
-    __device__ int probe(int mode, int one, uint32_t nsh, uint64_t sh, bool inval, int reply_len, int home,
+    __device__ __forceinline__ int probe(int mode, int one, uint32_t nsh, uint64_t sh, bool inval, int reply_len, int home,
                          const Req& r, int64_t timer, int delay) {
         constexpr int last = NL - 1;
         const bool single = mode == PR_ONE;
@@ -1676,13 +1685,13 @@ struct Engine {
         }
         return no_hops ? 2 : 1;
     }
-    __device__ int access_home(int cid, int home, const Req& r, int64_t timer, uint32_t* out_state, int staged = 0) {
+    __device__ __forceinline__ int access_home(int cid, int home, const Req& r, int64_t timer, uint32_t* out_state, int staged = 0) {
         PROF_T(p0);
         int d = access_home_impl(cid, home, r, timer, out_state, staged);
         PROF_ADD(PF_HOME, p0);
         return d;
     }
-    __device__ int access_home_impl(int cid, int home, const Req& r, int64_t timer, uint32_t* out_state,
+    __device__ __forceinline__ int access_home_impl(int cid, int home, const Req& r, int64_t timer, uint32_t* out_state,
                                     int staged) {
         PROF_T(p_ld);
         const DirGeo& D = g->dir;
@@ -1912,7 +1921,7 @@ struct Engine {
     // home transactions (write-back, request/reply, or the S->M upgrade) from
     // one loop, so the transmit and home-slice code is inlined once.
     template <int LV>
-    __device__ uint32_t mesi(int cid, const Req& r, int64_t timer) {
+    __device__ __forceinline__ uint32_t mesi(int cid, const Req& r, int64_t timer) {
         const LevelGeo& L = g->lv[LV];
         constexpr bool kLast = LV == NL - 1;
         LineMeta* meta = at<LineMeta>(OFF(L.off_meta));
@@ -2047,7 +2056,7 @@ struct Engine {
     // also creates every cache it snoops; a never-created cache holds no line
     // and mesi_bus discards the delays where that would show, so the engine
     // does not mark them.)
-    __device__ bool snoop(int cid, const Req& r, int mode) {
+    __device__ __forceinline__ bool snoop(int cid, const Req& r, int mode) {
         constexpr int last = NL - 1;
         const LevelGeo& L = g->lv[last];
         LineMeta* meta = at<LineMeta>(OFF(L.off_meta));
@@ -2086,7 +2095,7 @@ struct Engine {
     }
 
     template <int LV>
-    __device__ uint32_t mesi_bus(int cid, const Req& r, int64_t timer) {
+    __device__ __forceinline__ uint32_t mesi_bus(int cid, const Req& r, int64_t timer) {
         const LevelGeo& L = g->lv[LV];
         constexpr bool kLast = LV == NL - 1;
         LineMeta* meta = at<LineMeta>(OFF(L.off_meta));
@@ -2171,7 +2180,7 @@ struct Engine {
     // linear probing, no deletion: lane k reads slot h+k, so one round trip
     // covers 64 probe positions; the key is present iff it appears before the
     // first empty slot.
-    __device__ uint64_t page_translate(int prog, uint64_t vpage) {
+    __device__ __forceinline__ uint64_t page_translate(int prog, uint64_t vpage) {
         const TlbGeo& T = g->tlb;
         PageEnt* tab = at<PageEnt>(OFF(T.off_pages));
         const uint64_t mask = T.pages_cap - 1;
@@ -2207,7 +2216,7 @@ struct Engine {
 
     // System::tlb_translate (system.cpp:897-918): private TLB per core; the
     // request's address becomes physical (ppage << log2(page) | offset).
-    __device__ int tlb_translate(int core, Req& r, int64_t timer) {
+    __device__ __forceinline__ int tlb_translate(int core, Req& r, int64_t timer) {
         const TlbGeo& T = g->tlb;
         LineMeta* meta = at<LineMeta>(OFF(T.off_meta));
         int64_t* tsa = at<int64_t>(OFF(T.off_ts));
@@ -2241,7 +2250,7 @@ struct Engine {
     }
 
     // System::access (system.cpp:144-168).
-    __device__ int access(int core, const Req& r_in, int64_t timer) {
+    __device__ __forceinline__ int access(int core, const Req& r_in, int64_t timer) {
         if (core < 0 || core >= g->num_cores) {
             err_or(PU_ERRF_CORE_RANGE);
             return -1;
@@ -2259,7 +2268,7 @@ struct Engine {
         return dly;
     }
 
-    __device__ void flush_stats() {
+    __device__ __forceinline__ void flush_stats() {
         if (ln != 0) return;
         EngineStats* S = at<EngineStats>(OFF(g->off_stats));
         // Network::transmit's per-packet router term (hops+1)*router, inject
@@ -2315,6 +2324,23 @@ __device__ __forceinline__ int pool_next(uint32_t* sched, int cur) {
     if (lane_id() == 0) t = __hip_atomic_fetch_add(&sched[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int r = (int)rl32(t, 0);
     return r < (int)uni32((uint32_t)lds_pool.nrep) ? r : -1;
+}
+
+// Latency mode: the replica's queue headers (HBM lines of PU_HDR_PIECES
+// 16-B pieces) into / out of the LDS image (PU_LDS_SLOT pieces per queue:
+// a, b, c and the M/G/1 cache word d, which starts empty).  Thread t of the
+// two-wave workgroup copies slots t, t + 128, ...
+__device__ __forceinline__ void hdr_image_in(const char* qhdr, uint32_t nqueues, uint32_t t) {
+    const AS1 v4u32* gh = (const AS1 v4u32*)(AS1 char*)qhdr;
+    const uint32_t nq4 = nqueues * PU_LDS_SLOT;
+    for (uint32_t k = t; k < nq4; k += 128)
+        lds_qhdr[k] = (k & 3u) < 3u ? gh[(k >> 2) * PU_HDR_PIECES + (k & 3u)] : v4u32{~0u, ~0u, 0u, 0u};
+}
+__device__ __forceinline__ void hdr_image_out(char* qhdr, uint32_t nqueues, uint32_t t) {
+    AS1 v4u32* gh = (AS1 v4u32*)(AS1 char*)qhdr;
+    const uint32_t nq4 = nqueues * PU_LDS_SLOT;
+    for (uint32_t k = t; k < nq4; k += 128)
+        if ((k & 3u) < 3u) gh[(k >> 2) * PU_HDR_PIECES + (k & 3u)] = lds_qhdr[k];
 }
 
 // One replica's message loop (prime.cpp:120-137): reqs[b .. end) in order, D
@@ -2442,6 +2468,54 @@ __device__ __forceinline__ void replica_close(Engine<NL, LH>& e) {
 #endif
 }
 
+// One replica on this wave: replica `rep` runs requests [pos[ix] or off[ix],
+// off[ix+1]) (replica_loop) and its state goes back (replica_close); in
+// latency mode with the queue-header image in LDS around the loop (the
+// workgroup's helper wave runs mg1_helper meanwhile, uncore_body).  Returns
+// whether the range is done.
+template <int NL, int MODE, bool LH>
+__device__ __forceinline__ bool replica_run(Engine<NL, LH>& e, char* __restrict__ arena, int rep, int ix,
+                                            const pu_req* __restrict__ reqs, const uint64_t* __restrict__ off,
+                                            int32_t* __restrict__ delays, uint64_t* __restrict__ pos,
+                                            uint64_t deadline, uint32_t flags) {
+    constexpr bool SLICED = MODE >= 1;
+    // (pointer arithmetic on the kernel argument: the compiler keeps it a
+    // global-memory pointer, so the engine's accesses stay global_*, not flat_*)
+    e.base = arena + (size_t)rep * OFF(e.g->replica_bytes);
+    if constexpr (LH) {
+        // Latency mode: a two-wave workgroup; the helper wave (the second,
+        // uncore_body) copies the other half of the queue-header image.  The
+        // simulating wave copies slots lane, lane + 128, ... of the replica's
+        // queue headers into the LDS image (pieces a, b, c; d = no cached
+        // wait) before [1].
+        hdr_image_in(e.base + OFF(e.g->off_qhdr), (uint32_t)e.g->nqueues, (uint32_t)e.ln);
+        if (e.ln == 0) {
+            lds_hq_head = 0;
+            lds_main_done = 0;
+        }
+    }
+#ifdef PU_PROF
+    const uint64_t blk_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    const uint64_t b = pos ? pos[ix] : off[ix], end = off[ix + 1];
+    const bool done = replica_loop<NL, SLICED, LH>(e, reqs, delays, b, end, pos ? pos + ix : nullptr, deadline, flags);
+    if constexpr (LH) {                                   // the headers back
+        if (e.ln == 0) *(volatile AS3 uint32_t*)&lds_main_done = 1u;
+        __syncthreads();                                  // [2] the helper has stopped writing the image
+        hdr_image_out(e.base + OFF(e.g->off_qhdr), (uint32_t)e.g->nqueues, (uint32_t)e.ln);
+    }
+    replica_close<NL, LH>(e);
+#ifdef PU_PROF
+    if (e.ln == 0 && blockIdx.x < PU_PROF_BLOCKS) {
+        const uint64_t blk_t1 = __builtin_amdgcn_s_memrealtime();
+        g_blk_t0[blockIdx.x] = blk_t0;
+        g_blk_t1[blockIdx.x] = blk_t1;
+        g_blk_dur[blockIdx.x] += blk_t1 - blk_t0;
+    }
+#endif
+    return done;
+}
+
 // One workgroup (= one wavefront) per replica.  Replica replica0 + blockIdx.x
 // processes reqs[off[blockIdx.x] .. off[blockIdx.x+1]) in order (replica_loop).
 //
@@ -2483,83 +2557,46 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
     Engine<NL, LH> e;
     e.g = g;
     e.ln = lane_id();
-    // The replica this wave runs now; in a replica pool the wave's own state
-    // (the pool arguments, its replica) stays in LDS across the inlined
-    // engine, whose register budget is tight, and the one replica_loop call
-    // site below serves every replica the wave takes.
-    int r = replica0 + (int)blockIdx.x;
-    if constexpr (pool) {
+    if constexpr (LH) {
+        // the workgroup's second wave is the M/G/1 helper (the test is
+        // wave-uniform: readfirstlane tells the compiler so, and everything
+        // the simulating wave does after it stays uniform)
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 64) {
+            char* hb = arena + (size_t)(replica0 + (int)blockIdx.x) * OFF(g->replica_bytes) + OFF(g->off_qhdr);
+            hdr_image_in(hb, (uint32_t)g->nqueues, threadIdx.x);
+            __syncthreads();                              // [1] the image is in (stats_init's barrier)
+            mg1_helper();
+            __syncthreads();                              // [2] the main wave left its loop
+            hdr_image_out(hb, (uint32_t)g->nqueues, threadIdx.x);
+            __syncthreads();                              // [3] before the stats flush
+            return;
+        }
+    }
+    if constexpr (!pool) {
+        replica_run<NL, MODE, LH>(e, arena, replica0 + (int)blockIdx.x, (int)blockIdx.x, reqs, off, delays, pos,
+                                  deadline, flags);
+    } else {
+        // The replica pool: the wave's own state (the pool arguments, its
+        // replica) stays in LDS across the inlined engine, whose register
+        // budget is tight, and the one replica_run call site below serves
+        // every replica the wave takes.
         if (e.ln == 0) {
             lds_pool.nrep = nrep;
             lds_pool.r = (int32_t)sched[PU_POOL_SLOT0 + blockIdx.x] - 1;
         }
         __builtin_amdgcn_wave_barrier();
-        r = pool_next(sched, (int)uni32((uint32_t)lds_pool.r));
-    }
-    while (r >= 0) {
-        if (pool && e.ln == 0) lds_pool.r = r;
-        // (pointer arithmetic on the kernel argument: the compiler keeps it a
-        // global-memory pointer, so the engine's accesses stay global_*, not flat_*)
-        e.base = arena + (size_t)r * OFF(e.g->replica_bytes);
-        if constexpr (LH) {
-            // Latency mode: a two-wave workgroup.  Both waves copy the replica's
-            // queue headers into the LDS image (pieces a, b, c; d = no cached
-            // wait); wave 0 simulates, wave 1 is the M/G/1 helper (mg1_helper).
-            const AS1 v4u32* gh = (const AS1 v4u32*)(AS1 char*)(e.base + OFF(e.g->off_qhdr));
-            const uint32_t nq4 = (uint32_t)e.g->nqueues * PU_LDS_SLOT;
-            for (uint32_t k = threadIdx.x; k < nq4; k += 128)
-                lds_qhdr[k] = (k & 3u) < 3u ? gh[(k >> 2) * PU_HDR_PIECES + (k & 3u)] : v4u32{~0u, ~0u, 0u, 0u};
-            if (threadIdx.x == 0) {
-                lds_hq_head = 0;
-                lds_main_done = 0;
-            }
-            if (threadIdx.x >= 64) {                      // the helper wave
-                __syncthreads();                          // [1] stats_init's
-                mg1_helper();
-                __syncthreads();                          // [2] the main wave left its loop
-                AS1 v4u32* gho = (AS1 v4u32*)(AS1 char*)(e.base + OFF(e.g->off_qhdr));
-                for (uint32_t k = threadIdx.x; k < nq4; k += 128)
-                    if ((k & 3u) < 3u) gho[(k >> 2) * PU_HDR_PIECES + (k & 3u)] = lds_qhdr[k];
-                __syncthreads();                          // [3] before the stats flush
-                return;
-            }
+        int r = pool_next(sched, (int)uni32((uint32_t)lds_pool.r));
+        while (r >= 0) {
+            if (e.ln == 0) lds_pool.r = r;
+            // off[] and pos[] are indexed by replica in a pool
+            if (!replica_run<NL, MODE, LH>(e, arena, r, r, reqs, off, delays, pos, deadline, flags)) break;
+            r = pool_next(sched, -1);                     // its range is done: take the next
+            if (r < 0 && e.ln == 0) lds_pool.r = -1;
         }
-#ifdef PU_PROF
-        const uint64_t blk_t0 = __builtin_amdgcn_s_memrealtime();
-#endif
-        // the range: off[] and pos[] are indexed by replica in a pool, by
-        // workgroup otherwise
-        const int ix = pool ? r : (int)blockIdx.x;
-        const uint64_t b = pos ? pos[ix] : off[ix], end = off[ix + 1];
-        const bool done = replica_loop<NL, SLICED, LH>(e, reqs, delays, b, end, pos ? pos + ix : nullptr, deadline,
-                                                       flags);
-        if constexpr (LH) {                               // the headers back
-            if (e.ln == 0) *(volatile AS3 uint32_t*)&lds_main_done = 1u;
-            __syncthreads();                              // [2]
-            AS1 v4u32* gh = (AS1 v4u32*)(AS1 char*)(e.base + OFF(e.g->off_qhdr));
-            const uint32_t nq4 = (uint32_t)e.g->nqueues * PU_LDS_SLOT;
-            for (uint32_t k = threadIdx.x; k < nq4; k += 128)
-                if ((k & 3u) < 3u) gh[(k >> 2) * PU_HDR_PIECES + (k & 3u)] = lds_qhdr[k];
+        if (e.ln == 0) {
+            sched[PU_POOL_SLOT0 + blockIdx.x] = (uint32_t)(lds_pool.r + 1);
+            sched[PU_POOL_SLOT0 + gridDim.x + blockIdx.x] += (uint32_t)(__builtin_amdgcn_s_memrealtime() - wave_t0);
         }
-        replica_close<NL, LH>(e);
-#ifdef PU_PROF
-        if (e.ln == 0 && blockIdx.x < PU_PROF_BLOCKS) {
-            const uint64_t blk_t1 = __builtin_amdgcn_s_memrealtime();
-            g_blk_t0[blockIdx.x] = blk_t0;
-            g_blk_t1[blockIdx.x] = blk_t1;
-            g_blk_dur[blockIdx.x] += blk_t1 - blk_t0;
-        }
-#endif
-        if (!pool) break;
-        // a pool wave: keep the replica if the slice ran out, else take the next
-        if (!done) break;
-        r = pool_next(sched, -1);
-        if (r < 0 && e.ln == 0) lds_pool.r = -1;
-    }
-    if (pool && e.ln == 0) {
-        uint32_t* S = sched;
-        S[PU_POOL_SLOT0 + blockIdx.x] = (uint32_t)(lds_pool.r + 1);
-        S[PU_POOL_SLOT0 + gridDim.x + blockIdx.x] += (uint32_t)(__builtin_amdgcn_s_memrealtime() - wave_t0);
     }
 }
 
