@@ -1188,7 +1188,58 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
 // piece a (n), then b, then a again (the main wave writes a after b and c)
 // and stores only when the two reads of a agree.
 // Returns once the main wave has left its loop and every id is processed.
-__device__ void mg1_helper() {
+// Latency mode, the helper wave while it has no M/G/1 work (one simulation
+// alone +3.4% open loop, +0.4% closed loop, same-box A/B,
+// profiles/r4e_ab_single.txt): pull the lines
+// the simulating wave will load for its next PU_PF_AHEAD requests toward this
+// CU (its vector L1 and the XCD's L2): the request record, the requesting
+// core's L1 set (tags/state and timestamps) and the home directory set.  Only
+// loads (into a scratch LDS area, by LDS-DMA: no register of this wave waits
+// for them, and the simulating wave's own vmcnt never sees them); the
+// simulating wave reads everything again itself, so a prefetch can only be
+// early, never wrong.  `cur` (lds_ctl.cur) is read as a hint and clamped.
+#ifndef PU_PF_AHEAD
+#define PU_PF_AHEAD 4
+#endif
+static __shared__ uint32_t lds_pf_junk[64];
+__device__ __forceinline__ void pf_requests(const Geo* __restrict__ g, const char* base, const pu_req* reqs,
+                                            uint64_t first, uint32_t n) {
+    const int ln = lane_id();
+    const uint32_t j = (uint32_t)ln >> 3, k = (uint32_t)ln & 7u;
+    const bool mine = j < n;
+    uint64_t addr = 0;
+    int core = 0;
+    if (mine) {
+        const pu_req q = reqs[first + j];
+        addr = q.addr;
+        core = q.core;
+    }
+    const char* p = nullptr;
+    if (mine && (uint32_t)core < (uint32_t)g->num_cores) {
+        const LevelGeo& L = g->lv[0];
+        const uint64_t set = set_index(addr, L.offbits, L.nsets);
+        const uint64_t line0 = ((uint64_t)(uint32_t)core * L.nsets + set) * L.nways;
+        if (k == 0) p = (const char*)(reqs + first + j);
+        else if (k <= 2) {
+            if ((k - 1) * 64 < L.nways * sizeof(LineMeta)) p = base + L.off_meta + line0 * sizeof(LineMeta) + (k - 1) * 64;
+        } else if (k == 3) p = base + L.off_ts + line0 * 8;
+        else if (g->sys_type == 0 && k <= 6 && (k - 4) * 64 < g->dir.nways * sizeof(DirLine)) {
+            const DirGeo& D = g->dir;
+            int hb = (int)((addr >> g->home_offbits) & (((uint64_t)1 << g->home_mask_bits) - 1));
+            if (hb >= g->N) hb &= (1 << (g->home_mask_bits - 1)) - 1;    // System::allocHomeId
+            const uint64_t ds = set_index(addr, D.offbits, D.nsets);
+            const uint64_t dl0 = ((uint64_t)(uint32_t)hb * D.csets + (ds >> D.cset_shift)) * D.nways;
+            p = base + D.off_line + dl0 * sizeof(DirLine) + (k - 4) * 64;
+        }
+    }
+    if (p) lds_dma<false>((const AS1 char*)p, lds_addr(&lds_pf_junk[0]));
+}
+
+__device__ void mg1_helper(const Geo* __restrict__ g, const char* base, const pu_req* reqs, uint64_t b, uint64_t end) {
+    // no prefetch where the L1 probe is not on the request's own address
+    const bool pf_on = !g->tlb_enable;
+    uint64_t pf = b;                              // first request not yet prefetched
+
     const int ln = lane_id();
     uint32_t tail = 0;
     for (;;) {
@@ -1197,6 +1248,18 @@ __device__ void mg1_helper() {
             if (uni32(*(volatile AS3 uint32_t*)&lds_main_done)) {
                 if (uni32(*(volatile AS3 uint32_t*)&lds_hq_head) == tail) break;
                 continue;
+            }
+            if (pf_on) {
+                const uint64_t cur = uni64(*(volatile AS3 uint64_t*)&lds_ctl.cur);
+                if (cur >= b && cur < end) {
+                    const uint64_t lim = end - cur > PU_PF_AHEAD ? cur + 1 + PU_PF_AHEAD : end;
+                    if (pf <= cur) pf = cur + 1;
+                    if (pf < lim) {
+                        pf_requests(g, base, reqs, pf, (uint32_t)(lim - pf));
+                        pf = lim;
+                        continue;
+                    }
+                }
             }
             __builtin_amdgcn_s_sleep(1);
             continue;
@@ -1250,15 +1313,6 @@ struct Engine {
 
     template <class T>
     __device__ __forceinline__ T* at(uint64_t off) const {
-        if constexpr (LH) {
-            // latency kernel: the replica base made opaque at every use, so
-            // the compiler derives each region pointer where it is used
-            // instead of hoisting dozens of them out of the request loop
-            // (their SGPR pairs were spilled to VGPR lanes and reloaded)
-            AS1 char* b = (AS1 char*)base;
-            asm("" : "+s"(b));
-            return reinterpret_cast<T*>((char*)(b + off));
-        }
         return reinterpret_cast<T*>(base + off);
     }
 
@@ -2562,10 +2616,13 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
         // wave-uniform: readfirstlane tells the compiler so, and everything
         // the simulating wave does after it stays uniform)
         if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 64) {
-            char* hb = arena + (size_t)(replica0 + (int)blockIdx.x) * OFF(g->replica_bytes) + OFF(g->off_qhdr);
+            char* rb = arena + (size_t)(replica0 + (int)blockIdx.x) * OFF(g->replica_bytes);
+            char* hb = rb + OFF(g->off_qhdr);
             hdr_image_in(hb, (uint32_t)g->nqueues, threadIdx.x);
             __syncthreads();                              // [1] the image is in (stats_init's barrier)
-            mg1_helper();
+            const uint64_t rb0 = pos ? pos[blockIdx.x] : off[blockIdx.x];
+            mg1_helper(g, rb, reqs, rb0, off[blockIdx.x + 1]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no prefetch DMA outlives the wave
             __syncthreads();                              // [2] the main wave left its loop
             hdr_image_out(hb, (uint32_t)g->nqueues, threadIdx.x);
             __syncthreads();                              // [3] before the stats flush
