@@ -274,7 +274,7 @@ enum ProfId {
     PF_LOOP, PF_REQ, PF_NET, PF_NSETUP, PF_NHOPS, PF_NTREE, PF_NWAIT, PF_NWB, PF_SETL0, PF_SETLN, PF_HOME_LD,
     PF_HOME, PF_DOWN, PF_WINDOWS, PF_TREEHOPS, PF_DEMAND, PF_T_LDS, PF_T_SEARCH, PF_T_DECIDE, PF_T_EDIT,
     PF_T_STORE, PF_T_REFILL, PF_NPRE, PF_NPOST, PF_MG1RUN, PF_MG1LANES, PF_MG1HITS, PF_MAINTAIL,
-    PF_MG1PRESENT, PF_MG1STORED, PF_MG1BATCH, PF_COUNT
+    PF_MG1PRESENT, PF_MG1STORED, PF_MG1BATCH, PF_T_UPD, PF_COUNT
 };
 #ifdef PU_PROF
 static __shared__ unsigned long long lds_prof[PF_COUNT];
@@ -1018,6 +1018,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                 }
                 PROF_T(p_tree);
                 PROF_CNT(PF_TREEHOPS, 1);
+                PROF_T(p_pick);
                 const uint64_t tj = rl64(A, jt);
                 const int q = (int)rl32((uint32_t)rq, jt);
                 uint32_t head = rl32(vhead, jt), cnt = rl32(vcnt, jt);
@@ -1040,7 +1041,12 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                     PROF_CNT(PF_DEMAND, 1);
                     ring_load(c, q, head, cnt, v);
                 }
+#ifdef PU_PROF
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the ring's LDS read, in this region
+#endif
+                PROF_ADD(PF_T_LDS, p_pick);         // hop pick, DMA wait (NWAIT), ring from LDS
                 d = tree_op(c, q, v, head, cnt, tj, (uint64_t)plen, c.link_delay, err, f0n, f1n);
+                PROF_T(p_upd);
                 if (cnt >= PU_QMAX) {               // the next call's prune (history_tree.cpp:49-55), done now
                     head = (head + 1) & (PU_QRING - 1);
                     cnt--;
@@ -1063,6 +1069,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                 vfin = wl64(vfin, tj + d + (uint64_t)plen, jt);
                 t = tj + d + c.link_delay;
                 js = jt + 1;
+                PROF_ADD(PF_T_UPD, p_upd);          // prune, refill (T_REFILL), hop results into the window
                 PROF_ADD(PF_NTREE, p_tree);
             }
         } else {

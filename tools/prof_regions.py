@@ -20,7 +20,7 @@ PROF_LIB = os.environ.get("PROF_LIB") or os.path.join(ROOT, "primesim_amd", "lib
 NAMES = ["LOOP", "REQ", "NET", "NSETUP", "NHOPS", "NTREE", "NWAIT", "NWB", "SETL0", "SETLN", "HOME_LD",
          "HOME", "DOWN", "windows", "tree_hops", "demand_hops", "T_LDS", "T_SEARCH", "T_DECIDE", "T_EDIT",
          "T_STORE", "T_REFILL", "NPRE", "NPOST", "MG1RUN", "mg1_lanes", "mg1_cache_hits", "MAINTAIL",
-         "mg1_cache_present", "mg1_helper_stored", "mg1_helper_batches"]
+         "mg1_cache_present", "mg1_helper_stored", "mg1_helper_batches", "T_UPD"]
 COUNTS = {"windows", "tree_hops", "demand_hops", "mg1_lanes", "mg1_cache_hits", "mg1_cache_present",
           "mg1_helper_stored", "mg1_helper_batches"}
 
