@@ -340,7 +340,8 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
         del d_req
         log(f"[bench] {'closed' if replay else 'open'}-loop warmup step {s} done ({time.time() - t_w:.1f}s)")
     if os.environ.get("PU_PROF_RESET_AFTER_WARMUP"):   # tools/prof_regions.py: count the timed steps only
-        P.uncore.lib().pu_engine_prof_read(None, 0, 1)
+        L = P.uncore.lib()
+        (L.pu_jit_prof_read if os.environ.get("PU_PROF_JIT") else L.pu_engine_prof_read)(None, 0, 1)
     t_gen = time.time()
     W_t = steps * args.chunk
     d_win = torch.empty((R, W_t, REQ_BYTES), dtype=torch.uint8, device=dev)

@@ -253,6 +253,14 @@ int pu_compiled_config(const pu_handle* h);
  * of every code object it writes to the cache (cache maintenance keeps the
  * code objects whose prefix some library still carries). */
 const char* pu_jit_source_tag(void);
+
+/* Diagnostics, no reference counterpart (tools/prof_regions.py --jit): the
+ * region cycle counters of the loaded compiled-configuration kernels built
+ * with PRIMEUNCORE_JIT_EXTRA=-DPU_PROF, summed over modules into out[0..n);
+ * reset != 0 clears them.  Returns n, 0 when no loaded kernel counts regions,
+ * < 0 on error. */
+int pu_jit_prof_read(unsigned long long* out, int n, int reset);
+
 /* Return all replicas to the just-initialised state (no reallocation). */
 int        pu_reset(pu_handle* h);
 int        pu_num_replicas(const pu_handle* h);

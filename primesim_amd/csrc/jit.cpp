@@ -117,6 +117,18 @@ std::vector<std::string> options(const std::string& arch, int waves_1level) {
                                   "-DPU_JIT_GEO=\"pu_jit_geo.h\"", "-Wno-c99-designator",
                                   "-Werror=missing-field-initializers"};
     if (waves_1level > 0) o.push_back("-DPU_WAVES_1LEVEL=" + std::to_string(waves_1level));
+    // diagnostics only (tools/salu_lines.py: -gline-tables-only); the options
+    // are part of the cache key, so such objects never stand in for the product's
+    if (const char* e = std::getenv("PRIMEUNCORE_JIT_EXTRA"); e && *e) {
+        std::string s = e;
+        for (size_t i = 0; i < s.size();) {
+            const size_t j = s.find(' ', i);
+            const std::string w = s.substr(i, j == std::string::npos ? std::string::npos : j - i);
+            if (!w.empty()) o.push_back(w);
+            if (j == std::string::npos) break;
+            i = j + 1;
+        }
+    }
     return o;
 }
 
@@ -165,6 +177,8 @@ int compile(const std::string& geo_src, const std::vector<std::string>& opts, st
 }
 
 std::mutex g_jit_mu;   // one compile at a time per process (hipRTC holds a lot of memory)
+std::mutex g_mods_mu;  // the loaded modules (jit_prof_read)
+std::vector<hipModule_t> g_mods;
 constexpr const char* kBuildArch = "gfx950";   // the library's own target (Makefile ARCH)
 
 }  // namespace
@@ -247,6 +261,8 @@ bool load_module(const std::vector<char>& code, JitKernels* out, std::string* wh
                 return false;
             }
     out->mod = mod;
+    std::lock_guard<std::mutex> lk(g_mods_mu);
+    g_mods.push_back(mod);
     return true;
 }
 }  // namespace
@@ -314,8 +330,46 @@ int jit_warm(const Geo& g, std::string* key_out) {
 }
 
 void jit_unload(JitKernels* k) {
-    if (k->mod) (void)hipModuleUnload(k->mod);
+    if (k->mod) {
+        {
+            std::lock_guard<std::mutex> lk(g_mods_mu);
+            for (size_t i = 0; i < g_mods.size(); i++)
+                if (g_mods[i] == k->mod) {
+                    g_mods.erase(g_mods.begin() + (long)i);
+                    break;
+                }
+        }
+        (void)hipModuleUnload(k->mod);
+    }
     *k = JitKernels{};
+}
+
+// Diagnostics: the region counters (g_prof) of every loaded module compiled
+// with -DPU_PROF (PRIMEUNCORE_JIT_EXTRA), summed; optionally cleared with the
+// per-block durations.  Returns n, or 0 when no loaded module has them.
+int jit_prof_read(unsigned long long* out, int n, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    std::lock_guard<std::mutex> lk(g_mods_mu);
+    std::vector<unsigned long long> buf;
+    bool any = false;
+    for (int i = 0; i < n; i++) out[i] = 0;
+    for (hipModule_t m : g_mods) {
+        hipDeviceptr_t p = nullptr;
+        size_t bytes = 0;
+        if (hipModuleGetGlobal(&p, &bytes, m, "g_prof") != hipSuccess || !p) continue;
+        any = true;
+        const size_t k = bytes / sizeof(unsigned long long);
+        buf.assign(k, 0);
+        if (hipMemcpyDtoH(buf.data(), p, bytes) != hipSuccess) return -1;
+        for (int i = 0; i < n && (size_t)i < k; i++) out[i] += buf[i];
+        if (reset) {
+            if (hipMemsetD8(p, 0, bytes) != hipSuccess) return -1;
+            hipDeviceptr_t q = nullptr;
+            if (hipModuleGetGlobal(&q, &bytes, m, "g_blk_dur") == hipSuccess && q && hipMemsetD8(q, 0, bytes) != hipSuccess)
+                return -1;
+        }
+    }
+    return any ? n : 0;
 }
 
 int jit_launch(const JitKernels& k, bool sliced, bool lds_headers, int nblocks, hipStream_t stream, const Geo* d_geo,

@@ -29,6 +29,7 @@ int jit_load(const Geo& g, JitKernels* out, bool verbose);
 // Compile into the cache without a GPU; 1 = already cached, 0 = compiled.
 int jit_warm(const Geo& g, std::string* key_out);
 void jit_unload(JitKernels* k);
+int jit_prof_read(unsigned long long* out, int n, int reset);
 int jit_launch(const JitKernels& k, bool sliced, bool lds_headers, int nblocks, hipStream_t stream, const Geo* d_geo,
                char* arena, int replica0, const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
                uint64_t budget_ticks, uint32_t flags, uint32_t* sched = nullptr, int nrep = 0);

@@ -539,6 +539,11 @@ const char* pu_jit_source_tag(void) {
     return tag.c_str();
 }
 
+int pu_jit_prof_read(unsigned long long* out, int n, int reset) {
+    if (n < 0 || (n > 0 && !out)) return pu::set_error(PU_EINVAL, "bad arguments");
+    return pu::jit_prof_read(out, n, reset);
+}
+
 long pu_config_geo_source(const pu_sim_cfg* cfg, char* buf, size_t cap) {
     if (!cfg) return pu::set_error(PU_EINVAL, "bad arguments");
     Geo geo;

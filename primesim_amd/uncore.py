@@ -59,6 +59,7 @@ def lib() -> C.CDLL:
         "pu_config_jit_warm": (C.c_int, [P(A.SimCfg)]),
         "pu_compiled_config": (C.c_int, [C.c_void_p]),
         "pu_jit_source_tag": (C.c_char_p, []),
+        "pu_jit_prof_read": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]),
         "pu_destroy": (None, [C.c_void_p]),
         "pu_reset": (C.c_int, [C.c_void_p]),
         "pu_num_replicas": (C.c_int, [C.c_void_p]),
@@ -131,6 +132,8 @@ def lib() -> C.CDLL:
                                           P(A.Stats), C.c_int]),
     }
     for name, (res, args) in sig.items():
+        if name == "pu_jit_prof_read" and not hasattr(L, name):
+            continue   # diagnostics only: libraries of older commits (same-box A/B variants) lack it
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

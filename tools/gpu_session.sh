@@ -16,7 +16,9 @@
 #   sq_single    the same for one simulation alone, open loop and closed loop (latency kernel)
 #   handoff      tools/probe/handoff: dependent hand-off latency between two waves
 #   tworank      bench.py --gpus 2 with both ranks on card 0 (gloo)
-#   regions_single  lone-wave region profiles (PU_PROF build, libprimeuncore_prof.so), open and closed loop
+#   regions_single  lone-wave region profiles of the shipped compiled-configuration latency kernel
+#                (-DPU_PROF through PRIMEUNCORE_JIT_EXTRA), open and closed loop
+#   regions_ens  the same for the throughput kernel at the headline's replica count
 #   ab_modes:V1,V2,...   interleaved same-box A/B of engine libraries (main = libprimeuncore.so, else
 #                libprimeuncore_V.so) in three regimes: headline, one simulation alone open / closed loop
 #   ab_single:V1,V2,...  the same, one simulation alone only
@@ -65,8 +67,10 @@ for S in "$@"; do
     handoff) timeout -k 10 120 tools/probe/handoff > ${O}_handoff.json 2> ${O}_handoff.log || exit 1;;
     tworank) PU_BENCH_DEVICE=0 timeout -k 10 300 $BENCH --gpus 2 --steps 3 --warmup 2 --no-cpu --dist-backend gloo > ${O}_two_rank.json 2> ${O}_two_rank.log || exit 1;;
     regions_single)
-      PROF_LIB=$PWD/primesim_amd/libprimeuncore_prof.so timeout -k 10 200 python tools/prof_regions.py -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras > ${O}_regions_single_open.txt 2>&1 || exit 1
-      PROF_LIB=$PWD/primesim_amd/libprimeuncore_prof.so timeout -k 10 200 python tools/prof_regions.py -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras --replay closed > ${O}_regions_single_closed.txt 2>&1 || exit 1;;
+      timeout -k 10 200 python tools/prof_regions.py --jit -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras > ${O}_regions_single_open.txt 2>&1 || exit 1
+      timeout -k 10 200 python tools/prof_regions.py --jit -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras --replay closed > ${O}_regions_single_closed.txt 2>&1 || exit 1;;
+    regions_ens)
+      timeout -k 10 300 python tools/prof_regions.py --jit -- --steps 3 --warmup 5 --no-cpu --no-extras > ${O}_regions_ens.txt 2>&1 || exit 1;;
     ab_modes:*) ab 2 "ens single closed" "${S#ab_modes:}" > ${O}_ab_modes.txt || exit 1;;
     ab_single:*) ab 2 "single closed" "${S#ab_single:}" > ${O}_ab_single.txt || exit 1;;
     ab_ens:*) ab 3 "ens" "${S#ab_ens:}" > ${O}_ab_ens.txt || exit 1;;

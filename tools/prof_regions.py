@@ -7,6 +7,10 @@ per-request loop.  Regions are inclusive (NET contains NSETUP/NHOPS/NWB, NHOPS
 contains NTREE, NTREE contains NWAIT, HOME contains the transmits it makes).
 
     python tools/prof_regions.py -- --steps 3 --warmup 1 --no-cpu
+    python tools/prof_regions.py --jit -- --replicas 1 ...   (the shipped
+        compiled-configuration kernels, latency mode included: the product
+        library with PRIMEUNCORE_JIT_EXTRA=-DPU_PROF, its own cache entry;
+        warm it first with the same environment: tools/jit_warm.py)
 """
 from __future__ import annotations
 
@@ -26,28 +30,32 @@ COUNTS = {"windows", "tree_hops", "demand_hops", "mg1_lanes", "mg1_cache_hits", 
 
 
 def main() -> None:
-    if not os.path.exists(PROF_LIB):
-        raise SystemExit(f"{PROF_LIB} missing: make -C primesim_amd/csrc prof")
-    os.environ["PRIMEUNCORE_LIB"] = PROF_LIB
-    # the region counters live in the library's own (ahead-of-time) kernels: a
-    # profiling build for one configuration's constant geometry is made with
-    # tools/build_exp.sh NAME "-DPU_PROF -DPU_FIXED_GEO=..." (PROF_LIB env)
-    os.environ["PRIMEUNCORE_JIT"] = "0"
+    jit = "--jit" in sys.argv[1:]
+    if jit:
+        # the compiled-configuration kernels with the counters compiled in
+        os.environ["PRIMEUNCORE_JIT_EXTRA"] = "-DPU_PROF"
+        os.environ["PU_PROF_JIT"] = "1"
+    else:
+        if not os.path.exists(PROF_LIB):
+            raise SystemExit(f"{PROF_LIB} missing: make -C primesim_amd/csrc prof")
+        os.environ["PRIMEUNCORE_LIB"] = PROF_LIB
+        # the ahead-of-time kernels of the profiling build
+        os.environ["PRIMEUNCORE_JIT"] = "0"
     os.environ["PU_PROF_RESET_AFTER_WARMUP"] = "1"
     sys.path.insert(0, ROOT)
-    args = [a for a in sys.argv[1:] if a != "--"]
+    args = [a for a in sys.argv[1:] if a not in ("--", "--jit")]
     import bench  # noqa: E402
     import primesim_amd.uncore as U  # noqa: E402
 
     sys.argv = ["bench.py", *args]
     bench.main()
     L = U.lib()
-    fn = L.pu_engine_prof_read
+    fn = L.pu_jit_prof_read if jit else L.pu_engine_prof_read
     fn.restype = C.c_int
     fn.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
     buf = (C.c_ulonglong * len(NAMES))()
-    if fn(buf, len(NAMES), 0) < 0:
-        raise SystemExit("pu_engine_prof_read failed")
+    if fn(buf, len(NAMES), 0) <= 0:
+        raise SystemExit("no region counters read (a kernel built with -DPU_PROF must have run)")
     vals = dict(zip(NAMES, (int(x) for x in buf)))
     loop = max(vals["LOOP"], 1)
     out = {}
@@ -56,7 +64,7 @@ def main() -> None:
     # per-replica balance: summed per-block durations of the timed launches and
     # the last launch's start/end spread (s_memrealtime ticks, 100 MHz)
     R = min(4096, bench.LAST_REPLICAS or 0)
-    if R:
+    if R and not jit:
         import numpy as np
         t0 = (C.c_ulonglong * R)()
         t1 = (C.c_ulonglong * R)()
