@@ -278,10 +278,14 @@ enum ProfId {
 };
 #ifdef PU_PROF
 static __shared__ unsigned long long lds_prof[PF_COUNT];
+}  // namespace
+// (outside the anonymous namespace: a compiled-configuration module exports
+// them by name, jit.cpp's jit_prof_read)
 __device__ unsigned long long g_prof[PF_COUNT];
 // per-replica (block) wall-clock stamps of the last launch and summed durations
 #define PU_PROF_BLOCKS 4096
 __device__ unsigned long long g_blk_t0[PU_PROF_BLOCKS], g_blk_t1[PU_PROF_BLOCKS], g_blk_dur[PU_PROF_BLOCKS];
+namespace {
 #define PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define PROF_ADD(id, t0) \
     do { if (lane_id() == 0) atomicAdd(&lds_prof[id], (unsigned long long)(__builtin_amdgcn_s_memtime() - (t0))); } while (0)

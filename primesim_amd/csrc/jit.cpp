@@ -356,7 +356,10 @@ int jit_prof_read(unsigned long long* out, int n, int reset) {
     for (hipModule_t m : g_mods) {
         hipDeviceptr_t p = nullptr;
         size_t bytes = 0;
-        if (hipModuleGetGlobal(&p, &bytes, m, "g_prof") != hipSuccess || !p) continue;
+        if (hipModuleGetGlobal(&p, &bytes, m, "g_prof") != hipSuccess || !p) {
+            (void)hipGetLastError();   // not a profiling module: leave no error behind for the caller's runtime
+            continue;
+        }
         any = true;
         const size_t k = bytes / sizeof(unsigned long long);
         buf.assign(k, 0);
@@ -365,8 +368,8 @@ int jit_prof_read(unsigned long long* out, int n, int reset) {
         if (reset) {
             if (hipMemsetD8(p, 0, bytes) != hipSuccess) return -1;
             hipDeviceptr_t q = nullptr;
-            if (hipModuleGetGlobal(&q, &bytes, m, "g_blk_dur") == hipSuccess && q && hipMemsetD8(q, 0, bytes) != hipSuccess)
-                return -1;
+            if (hipModuleGetGlobal(&q, &bytes, m, "g_blk_dur") != hipSuccess) (void)hipGetLastError();
+            else if (q && hipMemsetD8(q, 0, bytes) != hipSuccess) return -1;
         }
     }
     return any ? n : 0;
