@@ -179,6 +179,7 @@ int compile(const std::string& geo_src, const std::vector<std::string>& opts, st
 std::mutex g_jit_mu;   // one compile at a time per process (hipRTC holds a lot of memory)
 std::mutex g_mods_mu;  // the loaded modules (jit_prof_read)
 std::vector<hipModule_t> g_mods;
+std::vector<unsigned long long> g_prof_unloaded;   // region counters of profiling modules already unloaded
 constexpr const char* kBuildArch = "gfx950";   // the library's own target (Makefile ARCH)
 
 }  // namespace
@@ -338,6 +339,19 @@ void jit_unload(JitKernels* k) {
                     g_mods.erase(g_mods.begin() + (long)i);
                     break;
                 }
+            // a profiling module's counters outlive it (a handle closed before
+            // the counters are read)
+            hipDeviceptr_t p = nullptr;
+            size_t bytes = 0;
+            if (hipModuleGetGlobal(&p, &bytes, k->mod, "g_prof") != hipSuccess || !p) {
+                (void)hipGetLastError();
+            } else if (hipDeviceSynchronize() == hipSuccess) {
+                std::vector<unsigned long long> buf(bytes / sizeof(unsigned long long), 0);
+                if (hipMemcpyDtoH(buf.data(), p, bytes) == hipSuccess) {
+                    if (g_prof_unloaded.size() < buf.size()) g_prof_unloaded.resize(buf.size(), 0);
+                    for (size_t i = 0; i < buf.size(); i++) g_prof_unloaded[i] += buf[i];
+                }
+            }
         }
         (void)hipModuleUnload(k->mod);
     }
@@ -351,8 +365,9 @@ int jit_prof_read(unsigned long long* out, int n, int reset) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     std::lock_guard<std::mutex> lk(g_mods_mu);
     std::vector<unsigned long long> buf;
-    bool any = false;
-    for (int i = 0; i < n; i++) out[i] = 0;
+    bool any = !g_prof_unloaded.empty();
+    for (int i = 0; i < n; i++) out[i] = (size_t)i < g_prof_unloaded.size() ? g_prof_unloaded[i] : 0;
+    if (reset) g_prof_unloaded.clear();
     for (hipModule_t m : g_mods) {
         hipDeviceptr_t p = nullptr;
         size_t bytes = 0;
