@@ -772,23 +772,26 @@ __device__ __forceinline__ void net_coords(const NetCtx& c, int id, int& x, int&
 // link of hop h of the X-then-Y-then-Z route from (sx,sy,sz) to (rx,ry,rz),
 // computed branch-free across lanes (hops of one route take different ranges):
 // hop h < hx moves along x at (sy, sz), then along y at (rx, sz), then along z
-// at (rx, ry); a = the coordinate (or coordinate - 1 moving down), and the link
-// id is net_link's (network.cpp:213-307): 2-D a*(2w) + b with b = sy | rx + w,
-// 3-D (a*w + b)*(3w) + cc with (b, cc) = (sy, sz) | (sz, rx + w) | (rx, ry + 2w).
+// at (rx, ry); a = the coordinate (or coordinate - 1 moving down).  The record
+// index is ours, not getLink's numbering (only the edge -> record bijection is
+// observable): the edges of one row (x), column (y) or pillar (z) are
+// consecutive, so the hops of a route segment are consecutive records and two
+// neighbouring hops share a 128-B line of headers (a visit reads half a line
+// instead of a whole one) and the LDS image's slots of a window spread over the
+// banks.  2-D: x (sy*(w-1) + a), y (w(w-1) + rx*(w-1) + a); 3-D: x, y, z blocks
+// of w^2(w-1) each, (sz*w + sy), (sz*w + rx), (ry*w + rx) rows of w-1.
 __device__ __forceinline__ int net_route_link(const NetCtx& c, int h, int sx, int sy, int sz, int rx, int ry, int rz,
                                               int hx, int hy) {
-    const int w = c.w;
+    const int w = c.w, w1 = c.w - 1;
     const bool e = rx > sx, n = ry > sy, u = rz > sz;   // wave-uniform
     const bool inx = h < hx, iny = h < hx + hy;
     const int hy_ = h - hx, hz_ = h - hx - hy;
     const int ax = e ? sx + h : sx - h - 1;
     const int ay = n ? sy + hy_ : sy - hy_ - 1;
-    if (c.net_type != 1) return inx ? ax * (2 * w) + sy : ay * (2 * w) + rx + w;
+    if (c.net_type != 1) return inx ? sy * w1 + ax : (w + rx) * w1 + ay;
     const int az = u ? sz + hz_ : sz - hz_ - 1;
-    const int A = inx ? ax : iny ? ay : az;
-    const int B = inx ? sy : iny ? sz : rx;
-    const int CC = inx ? sz : iny ? rx + w : ry + 2 * w;
-    return (A * w + B) * (3 * w) + CC;
+    const int blk = w * w * w1;
+    return inx ? (sz * w + sy) * w1 + ax : iny ? blk + (sz * w + rx) * w1 + ay : 2 * blk + (ry * w + rx) * w1 + az;
 }
 
 // LDS staging ring for predicted tree hops: PU_RING_PF full link rings per wave
