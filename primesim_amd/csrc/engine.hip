@@ -305,9 +305,10 @@ namespace {
 // Delays are < 2^31 (checked at pu_create); the magics are < 2^32 for w >= 2
 // (a 1-node mesh never routes).
 struct NetCtx {
-    AS1 char* qhdr;            // the replica's queue headers
+    AS1 char* qhdr;            // the replica's queue headers: pieces {a, b} of every queue, then c
     AS1 char* qring;           // ... and rings
     uint32_t router, link_delay, inject;
+    uint32_t hdr_c;            // byte offset of the c pieces (nqueues x 32)
     int header_flits, data_width, w, net_type;
     uint32_t w_magic, w2_magic;
     int w2, blk_len, plen_blk;
@@ -316,8 +317,11 @@ struct NetCtx {
 __device__ __forceinline__ AS1 v2u64* q_ring(const NetCtx& c, int q) {
     return reinterpret_cast<AS1 v2u64*>(c.qring) + (size_t)q * PU_QRING;
 }
-__device__ __forceinline__ AS1 uint32_t* q_hdr(const NetCtx& c, int q) {
-    return reinterpret_cast<AS1 uint32_t*>(c.qhdr + (uint64_t)q * sizeof(QueueHdr));
+__device__ __forceinline__ AS1 v4u32* q_hdr_ab(const NetCtx& c, int q) {
+    return reinterpret_cast<AS1 v4u32*>(c.qhdr + (uint64_t)q * PU_HDR_AB);
+}
+__device__ __forceinline__ AS1 v4u32* q_hdr_c(const NetCtx& c, int q) {
+    return reinterpret_cast<AS1 v4u32*>(c.qhdr + c.hdr_c + (uint64_t)q * PU_HDR_C);
 }
 
 // Load the `cnt` live slots of ring q starting at `head` (lane l holds slots l
@@ -670,10 +674,10 @@ __device__ __forceinline__ void q_store_hdr(const NetCtx& c, int q, const QState
         if (ring_changed) H[2] = cc;
         H[0] = a;
     } else {
-        AS1 uint32_t* H = q_hdr(c, q);
-        *reinterpret_cast<AS1 v4u32*>(H) = a;
-        *reinterpret_cast<AS1 v4u32*>(H + 4) = b;
-        if (ring_changed) *reinterpret_cast<AS1 v4u32*>(H + 8) = cc;
+        AS1 v4u32* H = q_hdr_ab(c, q);
+        H[0] = a;
+        H[1] = b;
+        if (ring_changed) *q_hdr_c(c, q) = cc;
     }
 }
 
@@ -732,10 +736,10 @@ __device__ __forceinline__ void hdr_load(const NetCtx& c, int q, v4u32& a, v4u32
         b = H[1];
         cc = H[2];
     } else {
-        const AS1 v4u32* H = reinterpret_cast<const AS1 v4u32*>(q_hdr(c, q));
+        const AS1 v4u32* H = q_hdr_ab(c, q);
         a = H[0];
         b = H[1];
-        cc = H[2];
+        cc = *q_hdr_c(c, q);
     }
 }
 
@@ -883,6 +887,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
     AS1 char* base = (AS1 char*)(char*)uni64((uint64_t)base_in);
     c.qhdr = base + OFF(g->off_qhdr);
     c.qring = base + OFF(g->off_qring);
+    c.hdr_c = (uint32_t)g->nqueues * PU_HDR_AB;
     c.router = (uint32_t)g->router_delay;
     c.link_delay = (uint32_t)g->link_delay;
     c.inject = (uint32_t)g->inject_delay;
@@ -1335,6 +1340,7 @@ struct Engine {
         NetCtx c;
         c.qhdr = (AS1 char*)base + OFF(g->off_qhdr);
         c.qring = (AS1 char*)base + OFF(g->off_qring);
+        c.hdr_c = (uint32_t)g->nqueues * PU_HDR_AB;
         c.router = (uint32_t)g->router_delay;
         c.link_delay = (uint32_t)g->link_delay;
         c.inject = (uint32_t)g->inject_delay;
@@ -2400,15 +2406,22 @@ __device__ __forceinline__ int pool_next(uint32_t* sched, int cur) {
 // two-wave workgroup copies slots t, t + 128, ...
 __device__ __forceinline__ void hdr_image_in(const char* qhdr, uint32_t nqueues, uint32_t t) {
     const AS1 v4u32* gh = (const AS1 v4u32*)(AS1 char*)qhdr;
+    const AS1 v4u32* gc = gh + (size_t)nqueues * (PU_HDR_AB / 16);
     const uint32_t nq4 = nqueues * PU_LDS_SLOT;
-    for (uint32_t k = t; k < nq4; k += 128)
-        lds_qhdr[k] = (k & 3u) < 3u ? gh[(k >> 2) * PU_HDR_PIECES + (k & 3u)] : v4u32{~0u, ~0u, 0u, 0u};
+    for (uint32_t k = t; k < nq4; k += 128) {
+        const uint32_t q = k >> 2, p = k & 3u;
+        lds_qhdr[k] = p < 2u ? gh[q * 2 + p] : p == 2u ? gc[q] : v4u32{~0u, ~0u, 0u, 0u};
+    }
 }
 __device__ __forceinline__ void hdr_image_out(char* qhdr, uint32_t nqueues, uint32_t t) {
     AS1 v4u32* gh = (AS1 v4u32*)(AS1 char*)qhdr;
+    AS1 v4u32* gc = gh + (size_t)nqueues * (PU_HDR_AB / 16);
     const uint32_t nq4 = nqueues * PU_LDS_SLOT;
-    for (uint32_t k = t; k < nq4; k += 128)
-        if ((k & 3u) < 3u) gh[(k >> 2) * PU_HDR_PIECES + (k & 3u)] = lds_qhdr[k];
+    for (uint32_t k = t; k < nq4; k += 128) {
+        const uint32_t q = k >> 2, p = k & 3u;
+        if (p < 2u) gh[q * 2 + p] = lds_qhdr[k];
+        else if (p == 2u) gc[q] = lds_qhdr[k];
+    }
 }
 
 // One replica's message loop (prime.cpp:120-137): reqs[b .. end) in order, D
@@ -2710,14 +2723,13 @@ __global__ void init_queues_kernel(char* arena, uint64_t replica_bytes, uint64_t
     if (id >= total) return;
     uint64_t r = id / (uint64_t)nqueues, q = id % (uint64_t)nqueues;
     char* base = arena + r * replica_bytes;
-    QueueHdr* h = reinterpret_cast<QueueHdr*>(base + off_qhdr) + q;
-    h->head = 0;
-    h->count = 1;
-    h->n = 0;
-    h->sum = 0.0;
-    h->sum_sq = 0.0;
-    h->newest = 0;
-    h->f0 = 0;
+    uint64_t* ab = reinterpret_cast<uint64_t*>(base + off_qhdr + q * PU_HDR_AB);
+    for (int i = 0; i < 4; i++) ab[i] = 0;   // n, sum, sum_sq, newest
+    uint32_t* cc = reinterpret_cast<uint32_t*>(base + off_qhdr + (uint64_t)nqueues * PU_HDR_AB + q * PU_HDR_C);
+    cc[0] = 0;   // head
+    cc[1] = 1;   // count
+    cc[2] = 0;   // f0
+    cc[3] = 0;
     QueueSlot* ring = reinterpret_cast<QueueSlot*>(base + off_qring) + q * PU_QRING;
     ring[0] = QueueSlot{0ull, UINT64_MAX};
 }

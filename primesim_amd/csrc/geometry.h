@@ -86,16 +86,12 @@ struct DirLine {
 // Three 16-B pieces: a = {n, Σs} and b = {Σs², newest} change on every visit
 // (an M/G/1 visit writes back one aligned 32-B half line), c = {head, count,
 // f0} only when the visit edits the free-interval ring.
-struct QueueHdr {
-    double n;          // QueueModelMG1::_num_arrivals as an exact double (< 2^53; 0.0 is all-zero bits)
-    double sum;        // _sigma_service_time
-    double sum_sq;     // _sigma_service_time_square
-    uint64_t newest;   // _newest_arrival_time
-    uint32_t head;
-    uint32_t count;
-    uint64_t f0;       // ring[head].first: the tree's minimum key (the M/G/1 test)
-    uint64_t pad[2];   // one header per 64-B line: a visit reads and writes one line, not two
-};
+// In HBM the pieces are two arrays: {a, b} of every queue (32 B each, an
+// M/G/1 visit's read-modify-write of one aligned 32-B piece pair), then c of
+// every queue (16 B each): the consecutive queues of a route segment share
+// 128-B lines four (a, b) or eight (c) at a time.
+constexpr uint32_t PU_HDR_AB = 32, PU_HDR_C = 16;
+constexpr uint32_t PU_HDR_BYTES = PU_HDR_AB + PU_HDR_C;   // per queue
 
 struct QueueSlot {
     uint64_t first;
@@ -212,5 +208,3 @@ struct RunState {
     uint64_t limit_at;     // last launch: index (into its request array) of the first request that
                            // raised a PU_ERRF_LIMITS bit; UINT64_MAX if none did
 };
-static_assert(sizeof(QueueHdr) == 64, "QueueHdr is three 16-B pieces in a 64-B line");
-constexpr uint32_t PU_HDR_PIECES = (uint32_t)(sizeof(QueueHdr) / 16);   // 16-B pieces per header in HBM

@@ -264,7 +264,7 @@ int build_geo(const pu_sim_cfg* c, Geo* g, uint64_t pool_cap = 0) {
         T.off_cnt = lay.take((uint64_t)y.num_cores * 32);
         T.off_pages = lay.take(T.pages_cap * sizeof(PageEnt));
     }
-    g->off_qhdr = lay.take((uint64_t)g->nqueues * sizeof(QueueHdr));
+    g->off_qhdr = lay.take((uint64_t)g->nqueues * PU_HDR_BYTES);
     g->off_qring = lay.take((uint64_t)g->nqueues * PU_QRING * sizeof(QueueSlot));
     g->off_stats = lay.take(sizeof(EngineStats));
     g->off_completion = lay.take((uint64_t)y.num_cores * 8);
@@ -1259,7 +1259,7 @@ int pu_unit_network_run(int num_nodes, int net_type, int data_width, int header_
     g.nlinks = w > 1 ? (w - 1) * w * (net_type == 1 ? 3 * w : 2) : 0;
     g.nqueues = g.nlinks;
     Layout lay;
-    g.off_qhdr = lay.take((uint64_t)g.nqueues * sizeof(QueueHdr));
+    g.off_qhdr = lay.take((uint64_t)g.nqueues * PU_HDR_BYTES);
     g.off_qring = lay.take((uint64_t)g.nqueues * PU_QRING * sizeof(QueueSlot));
     g.off_stats = lay.take(sizeof(EngineStats));
     g.replica_bytes = align_up(lay.cur, 4096);
