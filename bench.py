@@ -69,8 +69,9 @@ LAUNCH_CMD = None       # rank command for launch_ranks (None: this file; tests 
 LAST_REPLICAS = 0       # replicas of the last main() run (tools/prof_regions.py)
 LAST_PER_REPLICA = None  # per-replica stat deltas of the timed steps (profiling runs only)
 METRIC = "simulated memory accesses/sec (uncore) at 1024 cores; % HBM roofline"
-LIMITER = ("instruction issue and dependent-load latency (profiles/r3r_sq.json: 26% of wave cycles issuing, "
-           "57% waiting on memory, 17% in issue stalls at 5 waves/SIMD), not HBM bandwidth")
+LIMITER = ("dependent-load latency and instruction issue (profiles/r4n_sq.json: 30% of wave cycles issuing, "
+           "48% waiting on memory, 22% in issue stalls at 5 waves/SIMD; fabric traffic under half of 8 TB/s), "
+           "not HBM bandwidth")
 REQ_BYTES = 32          # sizeof(pu_req)
 VARIANTS = {0: "ahead-of-time kernels (runtime geometry) for every launch",
             1: "ahead-of-time kernels for the replicas (throughput launches); the configuration compiled into "
