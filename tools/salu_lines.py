@@ -68,17 +68,17 @@ def functions(path: str) -> list[tuple[int, str]]:
 
 
 def compile_lines(preset: str) -> str:
-    d = tempfile.mkdtemp(prefix="pu_salu_")
-    env = dict(os.environ, PRIMEUNCORE_JIT_CACHE=d, PRIMEUNCORE_JIT_EXTRA="-gline-tables-only")
-    code = ("import ctypes as C, sys; sys.path.insert(0, %r); import primesim_amd as P; "
-            "from primesim_amd import config as CF, uncore; cfg = P.config_from_dict(CF.preset(%r)); "
-            "rc = uncore.lib().pu_config_jit_warm(C.byref(cfg)); sys.exit(0 if rc >= 0 else 1)") % (ROOT, preset)
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise SystemExit(r.stderr[-3000:])
-    (hsaco,) = glob.glob(os.path.join(d, "*.hsaco"))
-    return subprocess.run([OBJDUMP, "-d", "-l", "--no-show-raw-insn", hsaco], capture_output=True,
-                          text=True).stdout
+    with tempfile.TemporaryDirectory(prefix="pu_salu_") as d:
+        env = dict(os.environ, PRIMEUNCORE_JIT_CACHE=d, PRIMEUNCORE_JIT_EXTRA="-gline-tables-only")
+        code = ("import ctypes as C, sys; sys.path.insert(0, %r); import primesim_amd as P; "
+                "from primesim_amd import config as CF, uncore; cfg = P.config_from_dict(CF.preset(%r)); "
+                "rc = uncore.lib().pu_config_jit_warm(C.byref(cfg)); sys.exit(0 if rc >= 0 else 1)") % (ROOT, preset)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise SystemExit(r.stderr[-3000:])
+        (hsaco,) = glob.glob(os.path.join(d, "*.hsaco"))
+        return subprocess.run([OBJDUMP, "-d", "-l", "--no-show-raw-insn", hsaco], capture_output=True,
+                              text=True).stdout
 
 
 def tally(dis: str, kernel: str):
