@@ -36,6 +36,36 @@ def test_queue_model_long_random_gpu():
     np.testing.assert_array_equal(got, want)
 
 
+def test_queue_model_ring_rebase_gpu():
+    """Arrivals ~2^25 cycles apart: the live intervals' offsets outgrow a compact
+    ring's 32-bit range within a few hundred calls, so the ring re-bases again
+    and again (its span stays below 2^32); parity against the CPU
+    restatement on every delay."""
+    rng = np.random.default_rng(11)
+    n = 20000
+    t = np.cumsum(rng.integers(1 << 24, 1 << 26, n)).astype(np.uint64)
+    t = t + rng.integers(0, 1 << 20, n).astype(np.uint64)
+    p = rng.integers(1, 13, n).astype(np.uint64)
+    got, _ = unit_queue(1, t, p)
+    want, _ = O.cpuref_queue(1, t, p)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_queue_model_ring_turns_wide_gpu():
+    """Bursts separated by jumps of 2^33 cycles: the live intervals then span
+    more than 2^32 cycles and the compact ring turns wide (16-B slots) for
+    good; every delay against the CPU restatement."""
+    rng = np.random.default_rng(12)
+    n = 20000
+    steps = rng.integers(0, 3, n).astype(np.uint64)
+    steps[::700] += np.uint64(1 << 33)
+    t = (np.cumsum(steps) + rng.integers(0, 300, n)).astype(np.uint64)
+    p = rng.integers(1, 13, n).astype(np.uint64)
+    got, _ = unit_queue(1, t, p)
+    want, _ = O.cpuref_queue(1, t, p)
+    np.testing.assert_array_equal(got, want)
+
+
 @pytest.mark.parametrize("name", ["mesh4x4", "mesh8x8_r1", "mesh3d_4", "mesh_ns_12"])
 def test_network_golden_gpu(name):
     with open(os.path.join(GOLDEN, "network.json")) as f:
