@@ -51,14 +51,3 @@ def test_engine_header_modes(name, mode, monkeypatch):
     monkeypatch.setenv("PRIMEUNCORE_LDS_HEADERS", mode)
     test_engine_reproduces_reference(name)
 
-
-@pytest.mark.parametrize("name", ["c1_hot", "c4_allcores", "three_level", "c4_closed", "mesh3d"])
-@pytest.mark.parametrize("mode", ["0", "2"])
-def test_engine_wide_rings(name, mode, monkeypatch):
-    """Every ring started in the 16-B slot format (PRIMEUNCORE_RING_FORMAT=wide),
-    which compact rings fall back to when their live intervals span 2^32 - 1
-    cycles: the wide paths of the ring DMA, the LDS decode, the demand load and
-    the tree operation's store, in both header placements."""
-    monkeypatch.setenv("PRIMEUNCORE_RING_FORMAT", "wide")
-    monkeypatch.setenv("PRIMEUNCORE_LDS_HEADERS", mode)
-    test_engine_reproduces_reference(name)
