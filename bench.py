@@ -80,6 +80,7 @@ VARIANTS = {0: "ahead-of-time kernels (runtime geometry) for every launch",
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 SEED_BASE = 4
 STAGE_GROUP = 256       # replicas whose requests the host generates per staging copy
+BUSY_MIN = 0.95         # a replica pool busier than this kept every slot resident for the whole slice
 
 
 def log(*a):
@@ -97,6 +98,21 @@ def alg_bytes(st: dict, cfg) -> float:
     b += st["net_distance"] * 96.0
     b += st["dram_accesses"] * 8.0
     return b
+
+
+def busy_guard(pool) -> str | None:
+    """Why a replica-pool pass cannot be reported, or None.  While unstarted
+    replicas remain, every slot's wavefront is resident for the whole slice
+    (busy ~1); a busy fraction under BUSY_MIN means part of the grid was not
+    resident and waited for the first waves' slice to end: the launch took
+    two slices (round 4's six-wave kernel: exactly half the rate)."""
+    if not pool or pool["replicas_started"] >= pool["replicas"]:
+        return None          # the pool ran dry: idle slots are expected
+    if pool["busy_fraction"] < BUSY_MIN:
+        return (f"replica pool busy fraction {pool['busy_fraction']:.3f} < {BUSY_MIN} with "
+                f"{pool['replicas'] - pool['replicas_started']} replicas never started: the grid of "
+                f"{pool['wavefronts']} wavefronts was not all resident (pu_resident_replicas overstated)")
+    return None
 
 
 def sum_stats(um, replicas: int) -> dict:
@@ -139,9 +155,12 @@ def stream_spec(seed: int, n: int = 0):
 
 
 def reference_engine(cfg_xml: str, cfg, mode: int = 0):
+    """The timed CPU baseline: the reference uncore compiled in place without
+    the golden generator's counting wraps (oracle/_ref/libprime_ref_nowrap.so;
+    a wrap adds a call per link visit), else the restatement."""
     import oracle as O
-    kind = "reference" if O.ref_available() else "port"
-    eng = O.RefUncore(cfg_xml) if kind == "reference" else O.CpuRef(cfg)
+    kind = "reference" if O.ref_available(plain=True) else "port"
+    eng = O.RefUncore(cfg_xml, plain=True) if kind == "reference" else O.CpuRef(cfg)
     eng.set_mode(mode)
     return kind, eng
 
@@ -217,13 +236,24 @@ def _ensemble_worker(conn, cfg_xml: str, fill: int, n_timed: int, budget_s: floa
         conn.close()
 
 
-def parity_replicas(R: int, workers: int) -> list:
-    """Replicas the ensemble replays: spread over 0..R-1, the last one R-1."""
+def parity_replicas(R: int, workers: int, slots: int = 0) -> list:
+    """Replicas the ensemble replays: spread over the slot range 0..S-1 (the
+    last one S-1), S = slots when the replica pool runs (slots < R), else R.
+    With the pool, a quarter of the workers (at least one) take the first
+    spare replicas S, S+1, ...: the pool hands out spares in index order as
+    slot replicas halt, so those are the spares that start (mid-slice, on a
+    wavefront that finished another replica) — R-1 usually never does."""
     if workers <= 1 or R <= 1:
         return [0][:workers]
-    step = max(1, R // workers)
-    reps = [min(w * step, R - 1) for w in range(workers - 1)] + [R - 1]
-    return sorted(set(reps))
+    S = slots if 0 < slots < R else R
+    k_sp = min(max(1, workers // 4), R - S) if S < R else 0
+    spread = max(1, workers - k_sp)
+    if spread == 1:
+        reps = [0]
+    else:
+        step = max(1, S // spread)
+        reps = [min(w * step, S - 1) for w in range(spread - 1)] + [S - 1]
+    return sorted(set(reps) | set(range(S, S + k_sp)))
 
 
 class Ensemble:
@@ -246,8 +276,8 @@ class Ensemble:
             self.pipes.append(a)
             self.procs.append(p)
 
-    def assign(self, R: int) -> list:
-        self.replicas = parity_replicas(R, self.workers)
+    def assign(self, R: int, slots: int = 0) -> list:
+        self.replicas = parity_replicas(R, self.workers, slots)
         for k, c in enumerate(self.pipes):
             c.send(("replica", self.replicas[k]) if k < len(self.replicas) else ("stop",))
         self.pipes, dropped = self.pipes[:len(self.replicas)], self.pipes[len(self.replicas):]
@@ -280,7 +310,7 @@ class Ensemble:
         return {"value": n / el, "unit": "accesses/s", "cores": nw, "kind": kind,
                 "cpu_model": cpu_model(),
                 "sample": f"{nw} processes, one per host core of this job's share, each the "
-                          f"{'reference uncore compiled from /root/reference/src' if kind == 'reference' else kind} "
+                          f"{'reference uncore compiled from /root/reference/src, no counting wraps' if kind == 'reference' else kind} "
                           f"on one GPU replica's C4 stream (replicas {self.replicas[0]}..{self.replicas[-1]}, spread "
                           f"over the GPU's replicas) after an untimed {self.fill}-request fill, run concurrently for "
                           f"{self.budget:g} s: {n} requests in {el:.2f} s (wall {wall:.2f} s)",
@@ -395,7 +425,8 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
     pool_info = None
     if pool:
         sch = d_sched.cpu().numpy().view(np.uint32)
-        busy_s = float(sch[2 + slots:2 + 2 * slots].astype(np.float64).sum()) * 1e-8   # 100-MHz ticks
+        b0 = (3 + slots) & ~1                                       # PU_POOL_BUSY0: one uint64 per slot
+        busy_s = float(sch[b0:b0 + 2 * slots].view(np.uint64).astype(np.float64).sum()) * 1e-8   # 100-MHz ticks
         started = int(min(int(sch[0]), R))
         pool_info = {"wavefronts": slots, "replicas": R, "replicas_started": started,
                      "busy_fraction": busy_s / (slots * sum(kern_ms) / 1e3),
@@ -630,7 +661,7 @@ def main(argv=None) -> None:
     LAST_REPLICAS = R
     # the ensemble's replicas, spread over 0..R-1: their delays are checked
     # against the reference's bit for bit (replica 0 also by cpu_baseline)
-    keep = sorted(set(ens.assign(R)) | {0}) if ens is not None else ([0] if rank == 0 else [])
+    keep = sorted(set(ens.assign(R, D.slots)) | {0}) if ens is not None else ([0] if rank == 0 else [])
 
     # ---- headline: open-loop replay
     H = D.headline(args, rank, world, keep)
@@ -645,6 +676,9 @@ def main(argv=None) -> None:
 
     parity_ok = True
     result = None
+    busy_err = busy_guard(H.pool)
+    if busy_err:
+        log(f"[bench] {busy_err}")
     if rank == 0:
         ens_res = ens.run() if ens is not None else None
         replica_parity = None
@@ -656,10 +690,15 @@ def main(argv=None) -> None:
                 g = H.kept[r]
                 m = min(len(g), len(d_cpu))
                 per[str(r)] = {"requests_compared": m, "gpu_window_requests": int(H.adv[r]),
+                               "spare": bool(r >= D.slots),
                                "bit_identical": bool(np.array_equal(g[:m], d_cpu[:m]))}
+            # spares the pool started mid-slice and that ran requests of the timed window
+            spares_run = [int(k) for k, v in per.items() if v["spare"] and v["gpu_window_requests"] > 0]
             replica_parity = {"replicas": sorted(ens.delays), "count": len(per),
                               "requests_compared": sum(v["requests_compared"] for v in per.values()),
                               "bit_identical": all(v["bit_identical"] for v in per.values()),
+                              "spares_started_and_compared": spares_run,
+                              "covers_pool_handoff": bool(H.pool) and len(spares_run) > 0,
                               "per_replica": per,
                               "note": f"GPU delays of each replica (its {args.warmup * args.chunk}-request warmup, "
                                       f"then its timed window) against the {ens_res['kind']} uncore's on the same "
@@ -686,7 +725,7 @@ def main(argv=None) -> None:
                 c_cpu = {"value": n_cpu / el, "unit": "accesses/s", "cores": 1, "kind": kind, "cpu_model": cpu_model(),
                          "sample": f"replica 0's C4 stream replayed closed-loop: requests {w0}..{w0 + n_cpu} after an "
                                    f"untimed closed-loop fill of {w0}, single-threaded "
-                                   f"({'reference uncore compiled from /root/reference/src' if kind == 'reference' else 'oracle/cpu_ref restatement'}), "
+                                   f"({'reference uncore compiled from /root/reference/src, no counting wraps' if kind == 'reference' else 'oracle/cpu_ref restatement'}), "
                                    f"{el:.1f} s"}
                 log(f"[bench] closed-loop cpu baseline ({kind}): {n_cpu / el:.0f} accesses/s")
             closed = {"value": C.processed / C.elapsed, "unit": "accesses/s", "steps": C.steps,
@@ -700,6 +739,7 @@ def main(argv=None) -> None:
                       "single_instance": None}
             gd = C.kept[0]
             closed["mean_delay_cycles"] = float(gd[gd != 0].mean()) if (gd != 0).any() else 0.0
+            busy_err = busy_err or busy_guard(C.pool)
             log(f"[bench] closed loop: {closed['value']:.4g} accesses/s, halted {C.halted}, "
                 f"M/G/1 share {closed['mg1_share_of_link_visits']:.3f}")
         um.close()
@@ -725,7 +765,7 @@ def main(argv=None) -> None:
                    "sample": f"replica 0's C4 stream: requests {w0}..{w0 + n_cpu} (the GPU's timed window; the GPU "
                              f"ran {int(H.adv[0])} of them for replica 0), after an untimed fill of the {w0}-request "
                              f"warmup, single-threaded "
-                             f"({'reference uncore compiled from /root/reference/src' if kind == 'reference' else 'oracle/cpu_ref restatement'}), "
+                             f"({'reference uncore compiled from /root/reference/src, no counting wraps' if kind == 'reference' else 'oracle/cpu_ref restatement'}), "
                              f"{el:.1f} s; GPU delays bit-identical on all {m} requests compared: {parity}",
                    "parity": parity}
             log(f"[bench] cpu baseline ({kind}): {n_cpu / el:.0f} accesses/s; parity on {m} delays: {parity}")
@@ -806,6 +846,7 @@ def main(argv=None) -> None:
             "cpu_baseline_ensemble": ens_res,
             "replica_parity": replica_parity,
             "parity": parity_ok if (not args.no_cpu and world == 1) else None,
+            "busy_guard": busy_err or f"ok: replica-pool busy fraction >= {BUSY_MIN} (or the pool ran dry)",
         }
         print(json.dumps(result), flush=True)
     else:
@@ -819,6 +860,9 @@ def main(argv=None) -> None:
     if not parity_ok:
         log("[bench] PARITY FAILURE: GPU delays differ from the reference")
         sys.exit(1)
+    if busy_err:
+        log("[bench] RESIDENCY FAILURE: the timed launches were not one slice each; the rate is not valid")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

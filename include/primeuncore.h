@@ -271,9 +271,11 @@ uint64_t   pu_replica_bytes(const pu_handle* h);
  * up to 2 GiB) and shrinks it, with a message on stderr, only when the
  * requested replicas would not fit the device otherwise. */
 uint64_t   pu_replica_pool_bytes(const pu_handle* h);
-/* Replicas this configuration's engine kernel keeps resident on the device at
- * once (one wave each; registers and LDS bound it).  A launch over more
- * replicas runs in several rounds.  No reference counterpart (engine sizing). */
+/* Replicas this configuration's throughput kernels (time-sliced and replica
+ * pool) keep resident on the device at once (one wave each; registers and LDS
+ * bound it, LDS counted in the device's 1,280-B allocation units, which
+ * hipOccupancy understates).  A launch over more replicas runs in several
+ * rounds.  No reference counterpart (engine sizing). */
 int        pu_resident_replicas(const pu_handle* h);
 
 /* Thread -> core map (reference src/thread_sched.cpp:55-91; identical quirks:
@@ -360,11 +362,12 @@ int pu_run_device_sliced(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_o
  * within the same slice, so no wavefront idles while unstarted replicas
  * remain.  Per replica the results are those of pu_run_device_sliced (each
  * replica is processed in order, by one wavefront at a time).  d_sched:
- * pu_pool_words(slots) = 2 + 2*slots uint32 words of device memory, all 0
- * before the first launch of a pool run, the same slots for every launch of
- * it (word 0 = replicas taken so far; word 1 unused; then per slot its
- * replica + 1, then per slot the 100-MHz ticks its wavefronts have been
- * resident, summed over launches: the busy time of the pool).
+ * pu_pool_words(slots) = B + 2*slots uint32 words of device memory,
+ * B = (3 + slots) & ~1, all 0 before the first launch of a pool run, the same
+ * slots for every launch of it (word 0 = replicas taken so far; word 1
+ * unused; then per slot its replica + 1; from word B, per slot one uint64:
+ * the 100-MHz ticks its wavefronts have been resident, summed over launches:
+ * the busy time of the pool).
  * budget_us > 0. */
 int  pu_pool_slots(pu_handle* h);
 long pu_pool_words(int slots);

@@ -23,9 +23,11 @@ from primesim_amd import _abi as A
 HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_LIB = os.path.join(HERE, "libpu_oracle.so")
 REF_LIB = os.path.join(HERE, "_ref", "libprime_ref.so")
+REF_NOWRAP_LIB = os.path.join(HERE, "_ref", "libprime_ref_nowrap.so")   # no counting wraps: the CPU baseline
 
 _olib: Optional[C.CDLL] = None
 _rlib: Optional[C.CDLL] = None
+_rlib_plain: Optional[C.CDLL] = None
 
 
 def oracle_lib() -> C.CDLL:
@@ -55,16 +57,20 @@ def oracle_lib() -> C.CDLL:
     return _olib
 
 
-def ref_available() -> bool:
-    return os.path.exists(REF_LIB)
+def ref_available(plain: bool = False) -> bool:
+    return os.path.exists(REF_NOWRAP_LIB if plain else REF_LIB)
 
 
-def ref_lib() -> C.CDLL:
-    global _rlib
-    if _rlib is None:
-        if not ref_available():
-            raise RuntimeError(f"{REF_LIB} missing: run `make -C oracle ref` where /root/reference exists")
-        L = C.CDLL(REF_LIB)
+def ref_lib(plain: bool = False) -> C.CDLL:
+    """The reference uncore compiled in place: with the counting wraps (the
+    golden generator; every extra counter), or plain (no wraps: the CPU
+    baseline's timing; extra counters read 0)."""
+    global _rlib, _rlib_plain
+    if (_rlib_plain if plain else _rlib) is None:
+        path = REF_NOWRAP_LIB if plain else REF_LIB
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make -C oracle ref` where /root/reference exists")
+        L = C.CDLL(path)
         P = C.POINTER
         L.ref_create.restype = C.c_void_p
         L.ref_create.argtypes = [C.c_char_p, P(C.c_int)]
@@ -85,8 +91,11 @@ def ref_lib() -> C.CDLL:
         L.ref_network_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64,
                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
                                       C.c_char_p, C.c_char_p, C.c_size_t]
-        _rlib = L
-    return _rlib
+        if plain:
+            _rlib_plain = L
+        else:
+            _rlib = L
+    return _rlib_plain if plain else _rlib
 
 
 class CpuRef:
@@ -171,55 +180,56 @@ REF_COUNTER_NAMES = ("link_visits", "link_flits", "mg1_calls", "lockdown_calls",
 class RefUncore:
     """The reference's own System (compiled in place) + the prime.cpp loop."""
 
-    def __init__(self, xml_path: str):
+    def __init__(self, xml_path: str, plain: bool = False):
         err = C.c_int(0)
-        self._h = ref_lib().ref_create(xml_path.encode(), C.byref(err))
+        self._L = ref_lib(plain)     # plain: the build without the counting wraps (counters() reads 0)
+        self._h = self._L.ref_create(xml_path.encode(), C.byref(err))
         if not self._h:
             raise RuntimeError(f"reference XmlParser rejected {xml_path}")
         cfg = A.SimCfg()
-        ref_lib().ref_get_config(self._h, C.byref(cfg))
+        self._L.ref_get_config(self._h, C.byref(cfg))
         self.cfg = cfg
         self.num_cores = cfg.sys.num_cores
 
     def close(self):
         if self._h:
-            ref_lib().ref_destroy(self._h)
+            self._L.ref_destroy(self._h)
             self._h = None
 
     def __del__(self):
         self.close()
 
     def alloc_core(self, prog: int, thread: int) -> int:
-        return ref_lib().ref_alloc_core(self._h, prog, thread)
+        return self._L.ref_alloc_core(self._h, prog, thread)
 
     def run(self, reqs: np.ndarray) -> tuple[np.ndarray, int]:
         reqs = np.ascontiguousarray(reqs, dtype=A.REQ_DTYPE)
         d = np.zeros(len(reqs), dtype=np.int32)
-        rc = ref_lib().ref_run(self._h, reqs.ctypes.data, len(reqs), d.ctypes.data)
+        rc = self._L.ref_run(self._h, reqs.ctypes.data, len(reqs), d.ctypes.data)
         return d, int(rc)
 
     def completion(self) -> np.ndarray:
         out = np.zeros(self.num_cores, dtype=np.int64)
-        ref_lib().ref_completion(self._h, out.ctypes.data, self.num_cores)
+        self._L.ref_completion(self._h, out.ctypes.data, self.num_cores)
         return out
 
     def set_mode(self, mode: int) -> None:
-        ref_lib().ref_set_mode(self._h, mode)
+        self._L.ref_set_mode(self._h, mode)
 
     def report(self) -> str:
         fd, tmp = tempfile.mkstemp(suffix=".report")
         os.close(fd)
-        n = ref_lib().ref_report(self._h, tmp.encode(), None, 0)
+        n = self._L.ref_report(self._h, tmp.encode(), None, 0)
         fd, tmp = tempfile.mkstemp(suffix=".report")
         os.close(fd)
         buf = C.create_string_buffer(n + 1)
-        ref_lib().ref_report(self._h, tmp.encode(), buf, n + 1)
+        self._L.ref_report(self._h, tmp.encode(), buf, n + 1)
         return buf.value.decode()
 
     @staticmethod
     def counters() -> dict:
         out = (C.c_uint64 * 7)()
-        ref_lib().ref_counters(out)
+        ref_lib().ref_counters(out)     # the wrapped build's counters (golden generation)
         return dict(zip(REF_COUNTER_NAMES, [int(x) for x in out]))
 
 

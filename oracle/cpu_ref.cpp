@@ -38,6 +38,10 @@
 #include <utility>
 #include <vector>
 
+#ifdef CPUREF_TRACE
+void cpuref_trace_link(size_t link, bool tree, size_t intervals);   // defined by the analysis build
+#endif
+
 namespace {
 
 enum : uint8_t { I = 0, S = 1, E = 2, M = 3, V = 4, B = 5 };
@@ -363,7 +367,14 @@ struct Sys {
     }
     uint64_t hop(size_t li, uint64_t t, int plen) {
         st.link_flits += (uint64_t)plen;
+#ifdef CPUREF_TRACE   // analysis builds only (tools/reuse/tree_reuse.py): which link, which branch
+        const uint64_t m0 = st.mg1_calls;
+        const uint64_t d = queue_delay(links[li], t, (uint64_t)plen, link_delay, &st.mg1_calls);
+        cpuref_trace_link(li, st.mg1_calls == m0, links[li].iv.size());
+        return d + link_delay;
+#else
         return queue_delay(links[li], t, (uint64_t)plen, link_delay, &st.mg1_calls) + link_delay;
+#endif
     }
     uint64_t transmit(int src, int dst, int len, uint64_t timer) {
         if (src == dst) return 0;

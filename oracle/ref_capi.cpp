@@ -33,6 +33,10 @@
 static uint64_t g_link_visits, g_link_flits, g_mg1_calls, g_lockdown_calls,
     g_bus_accesses, g_transmits, g_dram_accesses;
 
+// (oracle/Makefile also links this shim without the wraps, REF_NOWRAP:
+// _ref/libprime_ref_nowrap.so, the plain reference timed as bench.py's CPU
+// baseline; its extra counters read 0)
+#ifndef REF_NOWRAP
 extern "C" {
 uint64_t __real__ZN4Link6accessEmi(void* self, uint64_t timer, int packet_len);
 uint64_t __wrap__ZN4Link6accessEmi(void* self, uint64_t timer, int packet_len) {
@@ -66,6 +70,7 @@ int __wrap__ZN4Dram6accessEP6InsMem(void* self, void* ins) {
     return __real__ZN4Dram6accessEP6InsMem(self, ins);
 }
 }
+#endif
 
 static void reset_counters() {
     g_link_visits = g_link_flits = g_mg1_calls = g_lockdown_calls = 0;

@@ -180,12 +180,43 @@ typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
 // transmit adds its six network sums at once (lanes 0-5); the router, link and
 // inject delay totals are derived from them at the flush (Network::transmit's
 // per-packet terms are linear in them, network.cpp:146-156).
+// The compiled configuration of a configuration without verbose_report
+// (Geo.cnt_sum) also keeps the per-level {ins, miss, evict, wb} sums here
+// (SN_CNT0 + 4 * level + k; levels 0-3, PU_CNT_DIR, PU_CNT_TLB) instead of
+// one device-scope atomic per event on a per-cache counter: those atomics
+// bypass the XCD's L2 to the memory side (4.55 per access at C4,
+// TCC_EA0_WRREQ_ATOMIC_DRAM_32B) and sit in the wave's in-order vector
+// memory queue.  Only the verbose report lists caches one by one
+// (system.cpp:1020-1069); the ahead-of-time kernels keep per-cache counters.
+#if defined(PU_JIT_GEO)
+constexpr bool kCntSum = kJitGeo.cnt_sum != 0;
+#else
+constexpr bool kCntSum = false;
+#endif
 enum StatId {
     SN_ACC, SN_DIST, SN_TOTAL, SN_PLEN, SN_FLITS, SN_MG1, SN_DRAM, SN_BUSCONT,
-    SN_LOCKDOWN, SN_BUSACC, SN_REQS, SN_BCAST, SN_ROWHIT, SN_ROWEMPTY, SN_ROWCONF, SN_BANKWAIT, SN_COUNT
+    SN_LOCKDOWN, SN_BUSACC, SN_REQS, SN_BCAST, SN_ROWHIT, SN_ROWEMPTY, SN_ROWCONF, SN_BANKWAIT, SN_CNT0
 };
+constexpr int SN_COUNT = SN_CNT0 + (kCntSum ? 24 : 0);
 constexpr uint32_t SN_NET_LANES = 0x3F;   // SN_ACC .. SN_MG1
 static __shared__ unsigned long long lds_stat[SN_COUNT];
+// kCntSum: caches this launch already marked alive (System::init_caches'
+// lazy creation, system.cpp:172-207), one bit per cache of every level, so
+// the alive word in HBM is stored on first touch only (when all levels'
+// caches fit 4,096 bits).
+#ifndef PU_ALIVE_LDS
+#define PU_ALIVE_LDS 1
+#endif
+#if defined(PU_JIT_GEO)
+constexpr int alive_base(int l) { return l <= 0 ? 0 : alive_base(l - 1) + kJitGeo.lv[l - 1].ncaches; }
+constexpr bool kAliveLds = kCntSum && PU_ALIVE_LDS && alive_base(PU_JIT_NL) <= 4096;
+constexpr int kAliveWords = kAliveLds ? (alive_base(PU_JIT_NL) + 31) / 32 : 1;
+#else
+constexpr int alive_base(int) { return 0; }
+constexpr bool kAliveLds = false;
+constexpr int kAliveWords = 1;
+#endif
+static __shared__ uint32_t lds_alive[kAliveWords];
 static __shared__ unsigned long long lds_err;
 // The message loop's state (uncore_kernel), lane 0 its writer.
 struct LoopCtl {
@@ -1042,6 +1073,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                     mc &= mc - 1;
                     PROF_T(p_wait);
                     const int newer = issued - consumed - 1;  // rings issued after this one, < PU_RING_PF
+                    static_assert(PU_RING_PF <= 3, "the three-way wait covers at most 2 newer staged rings");
                     if (newer <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     else if (newer == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
                     else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -1475,12 +1507,26 @@ struct Engine {
         // System::init_caches (system.cpp:172-207) creates the cache and its
         // ancestors on first touch; only the existence bit is observable.
         for (int k = l; k < NL; k++) {
-            if (ln == (cid & 63)) at<uint32_t>(OFF(g->lv[k].off_alive))[cid] = 1u;
+            if constexpr (kAliveLds) {
+                const uint32_t bit = (uint32_t)(alive_base(k) + cid), m = 1u << (bit & 31);
+                const uint32_t w = uni32(lds_alive[bit >> 5]);
+                if (!(w & m)) {                 // first touch in this launch
+                    if (ln == (cid & 63)) at<uint32_t>(OFF(g->lv[k].off_alive))[cid] = 1u;
+                    if (ln == 0) lds_alive[bit >> 5] = w | m;
+                }
+            } else {
+                if (ln == (cid & 63)) at<uint32_t>(OFF(g->lv[k].off_alive))[cid] = 1u;
+            }
             if (k + 1 < NL) cid = cid * g->lv[k].share / g->lv[k + 1].share;
         }
     }
+    // one {ins, miss, evict, wb} event of cache cid at level K (0-3,
+    // PU_CNT_DIR, PU_CNT_TLB): a per-level LDS sum (kCntSum) or the cache's
+    // own counter
+    template <int K>
     __device__ __forceinline__ void count(uint64_t off_cnt, int cid, int which) const {
-        gatomic_add_u64_lane0(at<uint64_t>(off_cnt) + (size_t)cid * 4 + which, 1ull);
+        if constexpr (kCntSum) stat_add(SN_CNT0 + 4 * K + which, 1);
+        else gatomic_add_u64_lane0(at<uint64_t>(off_cnt) + (size_t)cid * 4 + which, 1ull);
     }
 
     // Dram::access (dram.cpp:43-47) at cycle t for line address addr: the
@@ -1773,7 +1819,8 @@ struct Engine {
         constexpr int last = NL - 1;
         const int blk = (int)g->lv[last].block;
         DirLine* lines = at<DirLine>(OFF(D.off_line));
-        if (ln == (home & 63)) at<uint32_t>(OFF(D.off_alive))[home] = 1u;   // home_stat[home] = 1
+        // home_stat[home] = 1 (read by the verbose report only)
+        if (!kCntSum && ln == (home & 63)) at<uint32_t>(OFF(D.off_alive))[home] = 1u;
         const uint64_t set = set_index(r.addr, D.offbits, D.nsets);
         const uint64_t tag = r.addr >> (D.offbits + D.idxbits);
         const uint64_t line0 = (uint64_t)(((uint32_t)home * (uint32_t)D.csets + (uint32_t)(set >> D.cset_shift)) * (uint32_t)D.nways);
@@ -1838,7 +1885,7 @@ struct Engine {
             }
         }
         PROF_ADD(PF_HOME_LD, p_ld);
-        count(OFF(D.off_cnt), home, 0);
+        count<PU_CNT_DIR>(OFF(D.off_cnt), home, 0);
         int delay = D.access_time;
         uint32_t st, nsh;
         uint64_t sh;
@@ -1894,7 +1941,7 @@ struct Engine {
             }
             dir_sharers(ww, nsh, sh);
             if (old_st != ST_I) {
-                count(OFF(D.off_cnt), home, 2);
+                count<PU_CNT_DIR>(OFF(D.off_cnt), home, 2);
                 pr = Req{old_addr, old_prog, PU_RD};
                 if (old_st == ST_M || old_st == ST_E) {
                     pmode = PR_ONE;
@@ -1908,7 +1955,7 @@ struct Engine {
                 }
             }
             st = r.type == PU_WR ? ST_M : ST_E;
-            count(OFF(D.off_cnt), home, 1);
+            count<PU_CNT_DIR>(OFF(D.off_cnt), home, 1);
             release_set = true;
             miss_fill = true;
         } else if (way < 0) {
@@ -2013,7 +2060,7 @@ struct Engine {
             stat_add(SN_BUSCONT, (uint64_t)(int64_t)db);
             dly += db;
         }
-        if (!hit) count(OFF(L.off_cnt), cid, 0);
+        if (!hit) count<LV>(OFF(L.off_cnt), cid, 0);
         dly += L.access_time;
         int way = set_find(v, meta, tsa, L.nways, r.prog);
         PROF_ADD(LV == 0 ? PF_SETL0 : PF_SETLN, p_set);
@@ -2054,11 +2101,11 @@ struct Engine {
             int old_prog;
             way = set_replace(v, meta, tsa, L.nways, L.offbits, L.idxbits, r.prog, &old_st, &old_addr, &old_prog);
             if (old_st != ST_I) {
-                count(OFF(L.off_cnt), cid, 2);
+                count<LV>(OFF(L.off_cnt), cid, 2);
                 Req o{old_addr, old_prog, PU_RD};
                 dly += children<LV, true>(cid, o);
                 if (old_st == ST_M || old_st == ST_E) {
-                    count(OFF(L.off_cnt), cid, 3);
+                    count<LV>(OFF(L.off_cnt), cid, 3);
                     if constexpr (kLast) {
                         tx_wb = true;
                         wb_home = home_of(old_addr);
@@ -2110,7 +2157,7 @@ struct Engine {
             }
             set_state(v, meta, way, is_miss ? ret : ST_M);
         }
-        if (is_miss) count(OFF(L.off_cnt), cid, 1);
+        if (is_miss) count<LV>(OFF(L.off_cnt), cid, 1);
         return ret;
     }
 
@@ -2187,7 +2234,7 @@ struct Engine {
             dly += db;
         }
         dly += L.access_time;
-        if (!hit) count(OFF(L.off_cnt), cid, 0);
+        if (!hit) count<LV>(OFF(L.off_cnt), cid, 0);
         int way = set_find(v, meta, tsa, L.nways, r.prog);
         bool is_miss = false, call_parent = false;
         int snoop_mode = -1;
@@ -2241,7 +2288,7 @@ struct Engine {
             }
         }
         if (is_miss) {
-            count(OFF(L.off_cnt), cid, 1);
+            count<LV>(OFF(L.off_cnt), cid, 1);
             return ret;
         }
         children<LV, true>(cid, r);                          // write hit: inval_children, discarded
@@ -2298,7 +2345,7 @@ struct Engine {
         SetView v;
         set_load(v, meta, tsa, T.nsets, T.nways, T.offbits, T.idxbits, (uint64_t)core, r.addr);
         const uint64_t mypp = !wide(T.nways) && (uint64_t)ln < T.nways ? ppa[v.line0 + (uint64_t)ln] : 0ull;
-        count(OFF(T.off_cnt), core, 0);
+        count<PU_CNT_TLB>(OFF(T.off_cnt), core, 0);
         int d = T.access_time;
         int way = set_find(v, meta, tsa, T.nways, r.prog);
         uint64_t ppage;
@@ -2307,8 +2354,8 @@ struct Engine {
             uint64_t old_addr;
             int old_prog;
             way = set_replace(v, meta, tsa, T.nways, T.offbits, T.idxbits, r.prog, &old_st, &old_addr, &old_prog);
-            if (old_st != ST_I) count(OFF(T.off_cnt), core, 2);
-            count(OFF(T.off_cnt), core, 1);
+            if (old_st != ST_I) count<PU_CNT_TLB>(OFF(T.off_cnt), core, 2);
+            count<PU_CNT_TLB>(OFF(T.off_cnt), core, 1);
             set_state(v, meta, way, ST_V);
             ppage = page_translate(r.prog, r.addr >> T.offbits);
             if (ln == wl(v, way)) ppa[v.line0 + (uint64_t)way] = ppage;
@@ -2343,8 +2390,12 @@ struct Engine {
     }
 
     __device__ __forceinline__ void flush_stats() {
-        if (ln != 0) return;
         EngineStats* S = at<EngineStats>(OFF(g->off_stats));
+        if constexpr (kCntSum) {   // lane k: per-level sum k
+            const uint64_t v = ln < SN_COUNT - SN_CNT0 ? lds_stat[SN_CNT0 + ln] : 0ull;
+            if (v) atomic_add_u64(&S->lvl_cnt[0][0] + ln, v);
+        }
+        if (ln != 0) return;
         // Network::transmit's per-packet router term (hops+1)*router, inject
         // term and link remainder total - router - (plen-1) - inject, summed
         // (mod 2^64, as the per-packet sums are)
@@ -2376,6 +2427,8 @@ struct Engine {
 __device__ __forceinline__ void stats_init() {
     const int ln = lane_id();
     if (ln < SN_COUNT) lds_stat[ln] = 0;
+    if constexpr (kAliveLds)
+        for (int i = ln; i < kAliveWords; i += 64) lds_alive[i] = 0u;
 #ifdef PU_PROF
     if (ln < PF_COUNT) lds_prof[ln] = 0;
 #endif
@@ -2679,7 +2732,8 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
         }
         if (e.ln == 0) {
             sched[PU_POOL_SLOT0 + blockIdx.x] = (uint32_t)(lds_pool.r + 1);
-            sched[PU_POOL_SLOT0 + gridDim.x + blockIdx.x] += (uint32_t)(__builtin_amdgcn_s_memrealtime() - wave_t0);
+            reinterpret_cast<uint64_t*>(sched + PU_POOL_BUSY0(gridDim.x))[blockIdx.x] +=
+                __builtin_amdgcn_s_memrealtime() - wave_t0;
         }
     }
 }
@@ -2869,20 +2923,37 @@ extern "C" int pu_engine_launch(const Geo* d_geo, int num_levels, char* arena, i
     return hipGetLastError() == hipSuccess ? 0 : PU_EIO;
 }
 
-// Replicas (one-wave workgroups) of the time-sliced kernel resident per CU at
-// once: VGPRs and the LDS ring staging bound it.  A launch of more replicas
-// runs the rest only after resident ones finish their slice.
-extern "C" int pu_engine_occupancy(int num_levels, int* blocks_per_cu) {
-    int n = 0;
+// Replicas (one-wave workgroups) of the throughput kernel of launch mode
+// `mode` (1 time-sliced, 2 replica pool) resident per CU at once by
+// hipOccupancy (VGPRs and the LDS ring staging bound it), and the kernel's
+// static LDS bytes (uncore.cpp applies the device's LDS granularity).  A
+// launch of more replicas runs the rest only after resident ones finish.
+template <int NL>
+static hipError_t occ_of(int mode, int* n, int* lds) {
+    hipFuncAttributes a{};
+    hipError_t e;
+    if (mode == 2) {
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(n, uncore_kernel<NL, 2>, 64, 0);
+        if (e == hipSuccess) e = hipFuncGetAttributes(&a, (const void*)uncore_kernel<NL, 2>);
+    } else {
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(n, uncore_kernel<NL, 1>, 64, 0);
+        if (e == hipSuccess) e = hipFuncGetAttributes(&a, (const void*)uncore_kernel<NL, 1>);
+    }
+    *lds = (int)a.sharedSizeBytes;
+    return e;
+}
+extern "C" int pu_engine_occupancy(int num_levels, int mode, int* blocks_per_cu, int* lds_bytes) {
+    int n = 0, lds = 0;
     hipError_t e;
     switch (num_levels) {
-        case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<1, 1>, 64, 0); break;
-        case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<2, 1>, 64, 0); break;
-        case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<3, 1>, 64, 0); break;
-        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, uncore_kernel<4, 1>, 64, 0); break;
+        case 1: e = occ_of<1>(mode, &n, &lds); break;
+        case 2: e = occ_of<2>(mode, &n, &lds); break;
+        case 3: e = occ_of<3>(mode, &n, &lds); break;
+        case 4: e = occ_of<4>(mode, &n, &lds); break;
         default: return PU_EINVAL;
     }
     *blocks_per_cu = n;
+    *lds_bytes = lds;
     return e == hipSuccess ? 0 : PU_EIO;
 }
 

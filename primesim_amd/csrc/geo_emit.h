@@ -32,7 +32,7 @@ inline std::string geo_cxx(const Geo& g, const char* var = "kJitGeo") {
     I32(home_offbits); I32(home_mask_bits);
     I32(blk_len); I32(plen_blk);
     U64(w_magic); U64(w2_magic);
-    I32(w2); I32(_pad0);
+    I32(w2); I32(cnt_sum);
     U64(router_delay); U64(link_delay); U64(inject_delay);
 #undef I32
 #undef U64

@@ -105,7 +105,13 @@ struct EngineStats {
     int64_t total_num_broadcast;
     uint64_t link_flits, mg1_calls, lockdown_calls, bus_accesses, requests, error_flags;
     uint64_t dram_row_hits, dram_row_empty, dram_row_conflicts, dram_bank_wait;
+    // per-level {ins, miss, evict, wb} sums kept by the compiled configuration
+    // when Geo.cnt_sum (levels 0-3, [PU_CNT_DIR] the directory slices,
+    // [PU_CNT_TLB] the TLBs); the host adds them to the per-cache counters
+    uint64_t lvl_cnt[6][4];
 };
+#define PU_CNT_DIR 4
+#define PU_CNT_TLB 5
 
 // One DRAM bank of the opt-in bank model (pu_dram_cfg): the cycle it is free
 // again and its open page + 1 (0 = closed).  Zeroed at reset: every bank
@@ -162,7 +168,10 @@ struct Geo {
     int32_t home_offbits, home_mask_bits;
     int32_t blk_len, plen_blk;      // last-level block size and its packet length (header + ceil(blk/dw))
     uint64_t w_magic, w2_magic;     // ceil(2^32 / w), ceil(2^32 / w^2): node id -> mesh coordinates
-    int32_t w2, _pad0;              // (exact division by multiply-high for ids < 2^16)
+    int32_t w2;                     // (exact division by multiply-high for ids < 2^16)
+    int32_t cnt_sum;                // 1 (no verbose_report): the compiled configuration keeps per-level
+                                    // {ins, miss, evict, wb} sums (EngineStats.lvl_cnt) instead of per-cache
+                                    // counters, and no directory alive bits (only the verbose report lists them)
     uint64_t router_delay, link_delay, inject_delay;
     LevelGeo lv[4];
     DirGeo dir;
@@ -179,11 +188,13 @@ struct Geo {
 // Kernel flags (per launch).
 // Replica pool (pu_run_device_pool): the scheduling words shared by the host
 // and the kernel.  sched[0] = next unstarted replica (the queue head);
-// sched[PU_POOL_SLOT0 + w] = replica + 1 held by slot w (0 = none), then one
-// word per slot: the s_memrealtime ticks (100 MHz) its wavefronts have been
-// resident, summed over launches.  All zero = nothing started.
+// sched[PU_POOL_SLOT0 + w] = replica + 1 held by slot w (0 = none), then
+// (from the even word PU_POOL_BUSY0) one uint64 per slot: the s_memrealtime
+// ticks (100 MHz) its wavefronts have been resident, summed over launches
+// (64 bits: 32 would wrap after 43 s per slot).  All zero = nothing started.
 #define PU_POOL_SLOT0 2u
-#define PU_POOL_WORDS(slots) (PU_POOL_SLOT0 + 2u * (uint32_t)(slots))
+#define PU_POOL_BUSY0(slots) ((PU_POOL_SLOT0 + (uint32_t)(slots) + 1u) & ~1u)
+#define PU_POOL_WORDS(slots) (PU_POOL_BUSY0(slots) + 2u * (uint32_t)(slots))
 #define PU_KF_NOHALT   1u   // System::access semantics: no prime.cpp:130-134 stop (pu_access)
 #define PU_KF_MSGHALT  2u   // a negative running delay stops only that message's receive
                             // thread (pu_req.tag): the rest of the message and every later

@@ -402,10 +402,13 @@ int jit_launch(const JitKernels& k, bool sliced, bool lds_headers, int nblocks, 
     return e == hipSuccess ? 0 : PU_EIO;
 }
 
-int jit_occupancy(const JitKernels& k, int* blocks_per_cu) {
-    int n = 0;
-    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, k.f[1][0], 64, 0) != hipSuccess) return PU_EIO;
+int jit_occupancy(const JitKernels& k, int mode, int* blocks_per_cu, int* lds_bytes) {
+    hipFunction_t f = k.f[mode == 2 ? 2 : 1][0];
+    int n = 0, lds = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 64, 0) != hipSuccess) return PU_EIO;
+    if (hipFuncGetAttribute(&lds, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, f) != hipSuccess) return PU_EIO;
     *blocks_per_cu = n;
+    *lds_bytes = lds;
     return 0;
 }
 

@@ -33,6 +33,8 @@ int jit_prof_read(unsigned long long* out, int n, int reset);
 int jit_launch(const JitKernels& k, bool sliced, bool lds_headers, int nblocks, hipStream_t stream, const Geo* d_geo,
                char* arena, int replica0, const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
                uint64_t budget_ticks, uint32_t flags, uint32_t* sched = nullptr, int nrep = 0);
-int jit_occupancy(const JitKernels& k, int* blocks_per_cu);
+// One-wave workgroups of the throughput kernel of launch mode `mode` (1
+// time-sliced, 2 replica pool) per CU by hipOccupancy, and its static LDS bytes.
+int jit_occupancy(const JitKernels& k, int mode, int* blocks_per_cu, int* lds_bytes);
 
 }  // namespace pu

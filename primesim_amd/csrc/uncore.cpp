@@ -49,7 +49,7 @@ extern "C" int pu_engine_unit_network(const Geo* d_geo, char* base, const int32_
                                       hipStream_t s);
 extern "C" int pu_engine_init_queues(char* arena, uint64_t replica_bytes, uint64_t off_qhdr, uint64_t off_qring,
                                      int nqueues, int nreplicas, hipStream_t stream);
-extern "C" int pu_engine_occupancy(int num_levels, int* blocks_per_cu);
+extern "C" int pu_engine_occupancy(int num_levels, int mode, int* blocks_per_cu, int* lds_bytes);
 
 namespace pu {
 
@@ -97,6 +97,7 @@ int build_geo(const pu_sim_cfg* c, Geo* g, uint64_t pool_cap = 0) {
     g->tlb_enable = y.tlb_enable;
     g->dram_access_time = y.dram_access_time;
     g->bus_latency = y.bus_latency;
+    g->cnt_sum = y.verbose_report ? 0 : 1;   // per-level sums suffice unless the report lists every cache
     Layout lay;
     int nbus = 0;
     for (int l = 0; l < y.num_levels; l++) {
@@ -674,14 +675,36 @@ uint64_t pu_replica_pool_bytes(const pu_handle* h) {
     return h ? (uint64_t)h->geo.dir.pool_entries * ((uint64_t)h->geo.dir.nwords * 8 + 4) : 0;
 }
 
+namespace pu {
+// gfx950 hands LDS to workgroups in 1,280-B units out of a CU's 160 KB
+// (measured: tools/probe/residency.hip, profiles/r5a_residency.json — one-wave
+// workgroups of 6,144 / 7,152 / 8,192 / 16,384 / 32,768 B reside 25 / 21 /
+// 18 / 9 / 4 per CU, hipOccupancy says 26 / 22 / 20 / 10 / 5).  A time-sliced
+// launch whose grid exceeds the resident waves takes two slices: round 4's
+// six-wave kernel (7,152 B: 22 by hipOccupancy, 21 resident) ran at half rate.
+constexpr int kLdsGranule = 1280;
+int lds_limited_per_cu(int lds_bytes, int lds_per_cu) {
+    if (lds_bytes <= 0) return 1 << 30;
+    const int unit = (lds_bytes + kLdsGranule - 1) / kLdsGranule * kLdsGranule;
+    return lds_per_cu / unit;
+}
+}  // namespace pu
+
 int pu_resident_replicas(const pu_handle* h) {
     if (!h) return pu::set_error(PU_EINVAL, "null handle");
-    int per_cu = 0, cus = 0;
+    int cus = 0, lds_cu = 0, per_cu = 1 << 30;
     HIP_TRY(hipSetDevice(h->device), PU_ENODEV);
-    // the throughput kernel's occupancy (one wave per replica)
-    int rc = h->jit.ok && h->jit_throughput ? pu::jit_occupancy(h->jit, &per_cu)
-                                            : pu_engine_occupancy(h->geo.num_levels, &per_cu);
-    if (rc) return pu::set_error(rc, "occupancy query failed");
+    HIP_TRY(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, h->device), PU_EIO);
+    // both throughput launch kinds (time-sliced, replica pool: separate
+    // instantiations, each its own registers and LDS), one wave per replica
+    for (int mode = 1; mode <= 2; mode++) {
+        int n = 0, lds = 0;
+        int rc = h->jit.ok && h->jit_throughput ? pu::jit_occupancy(h->jit, mode, &n, &lds)
+                                                : pu_engine_occupancy(h->geo.num_levels, mode, &n, &lds);
+        if (rc) return pu::set_error(rc, "occupancy query failed");
+        n = std::min(n, pu::lds_limited_per_cu(lds, lds_cu));
+        per_cu = std::min(per_cu, n);
+    }
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device), PU_EIO);
     return per_cu * cus;
 }
@@ -929,7 +952,8 @@ int pu_stats_get(pu_handle* h, int replica, pu_stats* out) {
     out->total_num_broadcast = es.total_num_broadcast;
     out->num_levels = h->geo.num_levels;
     for (int l = 0; l <= h->geo.num_levels; l++) {
-        pu_level_stats a{0, 0, 0, 0};
+        const uint64_t* ls = es.lvl_cnt[l == h->geo.num_levels ? PU_CNT_DIR : l];
+        pu_level_stats a{ls[0], ls[1], ls[2], ls[3]};
         for (size_t i = 0; i < alive[l].size(); i++) {
             a.ins += cnt[l][i * 4 + 0];
             a.miss += cnt[l][i * 4 + 1];
@@ -941,7 +965,8 @@ int pu_stats_get(pu_handle* h, int replica, pu_stats* out) {
     }
     {
         const auto& tc = cnt[h->geo.num_levels + 1];
-        pu_level_stats t{0, 0, 0, 0};
+        const uint64_t* ls = es.lvl_cnt[PU_CNT_TLB];
+        pu_level_stats t{ls[0], ls[1], ls[2], ls[3]};
         for (size_t i = 0; i + 3 < tc.size(); i += 4) {
             t.ins += tc[i];
             t.miss += tc[i + 1];
@@ -1032,7 +1057,7 @@ long pu_report(pu_handle* h, int replica, int include_time, char* buf, size_t ca
     if (g.tlb_enable) {
         // system.cpp:990-1014 ("replaced" is never accumulated, Q16)
         const auto& tc = cnt[g.num_levels + 1];
-        uint64_t ins = 0, miss = 0;
+        uint64_t ins = es.lvl_cnt[PU_CNT_TLB][0], miss = es.lvl_cnt[PU_CNT_TLB][1];
         for (size_t i = 0; i + 3 < tc.size(); i += 4) {
             ins += tc[i];
             miss += tc[i + 1];
@@ -1066,7 +1091,9 @@ long pu_report(pu_handle* h, int replica, int include_time, char* buf, size_t ca
     o << "Total delay caused by bus contention: " << es.total_bus_contention << " cycles\n";
     o << "Total # of broadcast: " << (int)es.total_num_broadcast << "\n\n";
     for (int i = 0; i < g.num_levels; i++) {
-        uint64_t ins = 0, miss = 0, evict = 0, wb = 0;
+        // per-level sums (compiled configuration, Geo.cnt_sum) + per-cache
+        // counters of caches that exist (a counted cache always does)
+        uint64_t ins = es.lvl_cnt[i][0], miss = es.lvl_cnt[i][1], evict = es.lvl_cnt[i][2], wb = es.lvl_cnt[i][3];
         for (size_t j = 0; j < alive[i].size(); j++) {
             if (!alive[i][j]) continue;
             ins += cnt[i][j * 4 + 0];
@@ -1088,7 +1115,7 @@ long pu_report(pu_handle* h, int replica, int include_time, char* buf, size_t ca
     {
         const auto& dc = cnt[g.num_levels];
         const auto& da = alive[g.num_levels];
-        uint64_t ins = 0, miss = 0, evict = 0;
+        uint64_t ins = es.lvl_cnt[PU_CNT_DIR][0], miss = es.lvl_cnt[PU_CNT_DIR][1], evict = es.lvl_cnt[PU_CNT_DIR][2];
         for (size_t j = 0; j < da.size(); j++) {
             if (!da[j]) continue;
             ins += dc[j * 4 + 0];

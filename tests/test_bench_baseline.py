@@ -36,6 +36,28 @@ def test_parity_replicas_spread_to_the_last():
     assert bench.parity_replicas(1, 16) == [0]
 
 
+def test_parity_replicas_cover_the_pool_spares():
+    """With the replica pool (5,120 slots, 5,520 replicas) a quarter of the
+    workers take the first spares, which the pool starts as slot replicas
+    halt; the rest spread over the slots up to the last slot."""
+    reps = bench.parity_replicas(5520, 16, 5120)
+    assert len(reps) == 16 and reps[0] == 0
+    assert reps[-4:] == [5120, 5121, 5122, 5123] and reps[-5] == 5119
+    assert bench.parity_replicas(5121, 16, 5120)[-2:] == [5119, 5120]   # one spare only
+    assert bench.parity_replicas(5520, 2, 5120) == [0, 5120]
+
+
+def test_busy_guard_refuses_a_grid_that_was_not_resident():
+    """A replica pool whose slots were not all resident (busy fraction under
+    0.95 while unstarted replicas remained) took two slices per launch: the
+    bench must not report that rate.  A pool that ran dry may idle."""
+    pool = {"wavefronts": 5632, "replicas": 6192, "replicas_started": 5901, "busy_fraction": 0.5}
+    assert "not all resident" in bench.busy_guard(pool)
+    assert bench.busy_guard(dict(pool, busy_fraction=0.998)) is None
+    assert bench.busy_guard(dict(pool, replicas_started=6192)) is None
+    assert bench.busy_guard(None) is None
+
+
 def test_ensemble_returns_the_delays_of_its_replicas(tmp_path):
     """The ensemble processes (forked before the GPU is touched) are told their
     replicas afterwards and send back every delay they produced: the same

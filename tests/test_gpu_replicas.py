@@ -333,6 +333,8 @@ def test_replica_pool_runs_every_replica_exactly():
         got, launches, sched = _pool_run(um, host, n, slots, 300)
         assert launches > R // slots, "a 300-us slice should not cover a replica's 3000 requests"
         assert sched[0] >= R and np.all(sched[2:2 + slots] == 0)   # every replica taken, every slot idle
+        busy = sched[(3 + slots) & ~1:][:2 * slots].view(np.uint64)   # PU_POOL_BUSY0: 64-bit ticks per slot
+        assert np.all(busy > 0) and np.all(busy < (1 << 40))                 # every slot ran; no wrap or garbage
         for r in range(R):
             want, ref = _oracle_run(cfg, specs[r], host[r])
             np.testing.assert_array_equal(got[r], want, err_msg=f"replica {r}")

@@ -20,9 +20,13 @@
 #                (-DPU_PROF through PRIMEUNCORE_JIT_EXTRA), open and closed loop
 #   regions_ens  the same for the throughput kernel at the headline's replica count
 #   ab_modes:V1,V2,...   interleaved same-box A/B of engine libraries (main = libprimeuncore.so, else
-#                libprimeuncore_V.so) in three regimes: headline, one simulation alone open / closed loop
+#                libprimeuncore_V.so; V@FLAGS also sets PRIMEUNCORE_JIT_EXTRA=FLAGS, '+' for a space,
+#                and V#W sets PRIMEUNCORE_JIT_WAVES=W) in three regimes: headline, one simulation
+#                alone open / closed loop
 #   ab_single:V1,V2,...  the same, one simulation alone only
 #   ab_ens:V1,V2,...     the same, headline only (3 rounds)
+#   residency    tools/probe/residency: one-wave workgroups resident per CU by resource shape
+#   diag:V       one headline run (5+5 steps) of variant V (ab syntax) with its bench log kept
 #   ab_pool      headline with the replica pool (--spare-replicas 0.1) vs without (0), 3 interleaved rounds
 set -o pipefail
 T=$1; shift
@@ -31,6 +35,14 @@ mkdir -p gpurun_out
 O=gpurun_out/${T}
 BENCH="python bench.py"
 DRIVER="--steps 20 --warmup 5"
+
+variant_env() {   # V[#WAVES][@FLAGS]: library V (main = the product), compiled-configuration options
+  local v=$1 lib extra waves
+  lib=${v%%[@#]*}
+  case $v in *@*) extra=${v#*@}; export PRIMEUNCORE_JIT_EXTRA="${extra//+/ }";; esac
+  case $v in *#*) waves=${v#*#}; waves=${waves%%@*}; export PRIMEUNCORE_JIT_WAVES=$waves;; esac
+  if [ "$lib" != main ]; then export PRIMEUNCORE_LIB=$PWD/primesim_amd/libprimeuncore_$lib.so; fi
+}
 
 ab() {   # ab ROUNDS MODES VARIANTS
   local R=$1 MODES=$2 VARS=$3 mode v ARGS
@@ -42,7 +54,7 @@ ab() {   # ab ROUNDS MODES VARIANTS
         closed) ARGS="--replicas 1 --steps 3 --warmup 5 --no-cpu --no-extras --replay closed";;
       esac
       for v in ${VARS//,/ }; do
-        ( if [ "$v" != main ]; then export PRIMEUNCORE_LIB=$PWD/primesim_amd/libprimeuncore_$v.so; fi
+        ( variant_env "$v"
           timeout -k 10 200 $BENCH $ARGS 2>>${O}_ab.err | python -c "import json,sys; b=json.loads(sys.stdin.read().strip().splitlines()[-1]); v=b['value']; print('$mode', '$v', round(v) if v < 1e6 else round(v / 1e6, 2), flush=True)" ) || return 1
       done
     done
@@ -71,6 +83,9 @@ for S in "$@"; do
       timeout -k 10 200 python tools/prof_regions.py --jit -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras --replay closed > ${O}_regions_single_closed.txt 2>&1 || exit 1;;
     regions_ens)
       timeout -k 10 300 python tools/prof_regions.py --jit -- --steps 3 --warmup 5 --no-cpu --no-extras > ${O}_regions_ens.txt 2>&1 || exit 1;;
+    residency) timeout -k 10 120 tools/probe/residency > ${O}_residency.json 2> ${O}_residency.log || exit 1;;
+    diag:*) ( variant_env "${S#diag:}"
+              timeout -k 10 300 $BENCH --steps 5 --warmup 5 --no-cpu --no-extras > ${O}_diag.json 2> ${O}_diag.log ) || exit 1;;
     ab_modes:*) ab 2 "ens single closed" "${S#ab_modes:}" > ${O}_ab_modes.txt || exit 1;;
     ab_single:*) ab 2 "single closed" "${S#ab_single:}" > ${O}_ab_single.txt || exit 1;;
     ab_ens:*) ab 3 "ens" "${S#ab_ens:}" > ${O}_ab_ens.txt || exit 1;;

@@ -92,7 +92,18 @@ def main() -> int:
     stale = []
     if not bad and os.path.realpath(cache) == os.path.realpath(intree):
         live = live_source_tags()
-        for f in glob.glob(os.path.join(cache, "*.hsaco")):
+        # the product library's own tag, read in this process: if it is missing
+        # from what the children reported (a child load failed, a library
+        # lacks the symbol), nothing is pruned
+        from primesim_amd import uncore
+        own = uncore.lib().pu_jit_source_tag
+        own.restype = C.c_char_p
+        own_tag = own().decode()
+        if own_tag not in live:
+            print(f"[jit_warm] the product library's source tag {own_tag} was not among the tags read back "
+                  f"({sorted(live)}): nothing pruned", flush=True)
+            live = None
+        for f in glob.glob(os.path.join(cache, "*.hsaco")) if live else []:
             tag = os.path.basename(f).split("-")[0]
             if tag not in live and os.path.getmtime(f) < t0 - PRUNE_HOURS * 3600:
                 stale.append(f)
