@@ -40,6 +40,7 @@
 
 #ifdef CPUREF_TRACE
 void cpuref_trace_link(size_t link, bool tree, size_t intervals);   // defined by the analysis build
+static size_t g_trace_k;   // index (from the front) of the interval the last tree search stopped at
 #endif
 
 namespace {
@@ -84,6 +85,9 @@ uint64_t queue_delay(Queue& q, uint64_t t, uint64_t p, uint64_t min_proc, uint64
             const auto& x = v[k];
             if ((x.first <= t && t + p <= x.second) || (t < x.first && x.second - x.first >= p)) break;
         }
+#ifdef CPUREF_TRACE
+        g_trace_k = k;
+#endif
         auto& x = v[k];
         if (t >= x.first) {
             d = 0;
@@ -370,7 +374,7 @@ struct Sys {
 #ifdef CPUREF_TRACE   // analysis builds only (tools/reuse/tree_reuse.py): which link, which branch
         const uint64_t m0 = st.mg1_calls;
         const uint64_t d = queue_delay(links[li], t, (uint64_t)plen, link_delay, &st.mg1_calls);
-        cpuref_trace_link(li, st.mg1_calls == m0, links[li].iv.size());
+        cpuref_trace_link(li, st.mg1_calls == m0, g_trace_k);
         return d + link_delay;
 #else
         return queue_delay(links[li], t, (uint64_t)plen, link_delay, &st.mg1_calls) + link_delay;

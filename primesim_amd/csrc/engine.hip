@@ -147,13 +147,17 @@ struct RingView {
     uint64_t lf, ls, hf, hs;
 };
 
-// A queue header (QueueHdr dwords 0-13) as held by a lane.
+// A queue's state as held by a lane (hdr_state): the ring cursor, the M/G/1
+// moments (queue_model_m_g_1.cpp: _num_arrivals as an exact double, the
+// service-time sum and sum of squares), the newest finish time, the first
+// free-interval start; n0 / n1 are the packed header's visit counts.
 struct QState {
     uint32_t head, count;
     double n;           // _num_arrivals, held as an exact double (< 2^53)
     double sum, sum_sq;
     uint64_t newest;
     uint64_t f0;
+    uint64_t n0, n1;
 };
 
 #define AS1 __attribute__((address_space(1)))
@@ -336,10 +340,11 @@ namespace {
 // Delays are < 2^31 (checked at pu_create); the magics are < 2^32 for w >= 2
 // (a 1-node mesh never routes).
 struct NetCtx {
-    AS1 char* qhdr;            // the replica's queue headers: pieces {a, b} of every queue, then c
+    AS1 char* qhdr;            // the replica's queue headers (packed: 32 B each; wide: {a, b} of every queue, then c)
     AS1 char* qring;           // ... and rings
     uint32_t router, link_delay, inject;
-    uint32_t hdr_c;            // byte offset of the c pieces (nqueues x 32)
+    uint32_t hdr_c;            // wide headers: byte offset of the c pieces (nqueues x 32)
+    uint32_t p0, p1;           // packed headers: the two packet lengths the visit counts n0, n1 stand for
     int header_flits, data_width, w, net_type;
     uint32_t w_magic, w2_magic;
     int w2, blk_len, plen_blk;
@@ -652,79 +657,123 @@ __device__ __forceinline__ uint64_t selm64(uint64_t m, uint64_t a, uint64_t b) {
     const uint32_t lo = selm32(m, (uint32_t)a, (uint32_t)b), hi = selm32(m, (uint32_t)(a >> 32), (uint32_t)(b >> 32));
     return ((uint64_t)hi << 32) | lo;
 }
+// ---- queue headers ---------------------------------------------------------
+// The engine's header (PU_HDR_BYTES = 32 per queue, two 16-B pieces):
+//   a = {n0 | head << 48, n1 | count << 48}   b = {newest, f0}
+// n0 / n1 count the visits with packet length p0 / p1.  The engine sends only
+// two packet lengths over a link (0-byte messages: header_flits; blocks:
+// plen_blk, network.cpp:104) and one over a bus (bus_latency), so the M/G/1
+// moments of queue_model_m_g_1.cpp:45-55 follow from the counts:
+//   n = n0 + n1,  Σs = p0·n0 + p1·n1,  Σs² = p0²·n0 + p1²·n1
+// — the same doubles the reference accumulates (each partial sum is an
+// integer below 2^53, so every addition is exact; a moment reaching 2^53 sets
+// PU_ERRF_QUEUE, an engine limit past ~10^14 visits of one link).  The ring
+// cursor (head, count) rides in the top bits of a, the first interval start
+// f0 (the M/G/1 test) in b: one 32-B read-modify-write per visit, four
+// neighbouring hops of a route per 128-B line (round 4's 48-B header read a
+// second line of c pieces per four hops).
+// The unit hooks (any packet length: unit_queue_kernel, unit_network_kernel)
+// keep the wide header (WIDE, PU_HDR_WIDE_BYTES = 48: {a, b} of every queue,
+// then c of every queue): a = {n, Σs}, b = {Σs², newest} as doubles,
+// c = {head, count, f0}.
+//
 // Latency mode (LH): a launch with at most one replica per CU keeps every
 // queue header of its replica in the CU's LDS for the whole launch (copied in
 // at the start, back at the end), so the header round trip of each route
-// window becomes an LDS read.  136 KB: 2,176 queues (a 32x32 mesh has 1,984)
-// in 64-B slots: the header's three 16-B pieces a = {n, Σs},
-// b = {Σs², newest}, c = {head, count, f0}, then d = {M/G/1 cache, unused}.
+// window becomes an LDS read: PU_LDS_Q queues, a 32-B slot {a, b} each, plus
+// one 8-B M/G/1 cache word per queue (lds_qcache).
 //
 // The M/G/1 cache: the queue delay of an M/G/1 visit depends only on the
 // moments the link holds before the visit (queue_model_m_g_1.cpp:16-42), and
 // those change only when the link is visited.  In latency mode a second wave
 // of the workgroup (mg1_helper) recomputes the wait of every link a route
 // window just updated, on another SIMD, and stores it as
-// d.x = wait | (n ^ wait) << 32 (n < 2^32, waits < 2^32 - 1; larger ones
+// wait | (n ^ wait) << 32 (n < 2^32, waits < 2^32 - 1; larger ones
 // are not cached); the simulating wave uses it when the high half xor the
 // wait equals its header's n and computes the wait itself otherwise.  The tag
 // is n itself, not a residue, so a slot the helper skipped (it fell more than
 // PU_HQ ids behind) can never match a later visit; folding the wait into it
 // makes a read of the slot torn against the helper's write (old wait, new tag
-// or the reverse) fail the check unless both waits are equal.  The main wave writes piece a (which holds n) after b
-// and c; the helper reads a, then b, then a again and stores only when both
-// reads of a are bit-identical (Σs grows at every visit, so a read of a torn
-// against the main wave's write, or a b newer than a, shows as a mismatch):
-// a stored wait was computed from exactly the moments its tag names.
-#define PU_LDS_QHDR_BYTES (136 * 1024)
-#define PU_LDS_SLOT 4u                     // 16-B pieces per LDS header slot
+// or the reverse) fail the check unless both waits are equal.  The main wave
+// writes piece a (which holds n) after b; the helper reads a, then b, then a
+// again and stores only when both reads of a are bit-identical (n grows at
+// every visit, so a read of a torn against the main wave's write, or a b newer
+// than a, shows as a mismatch, and a wait computed from such a mix carries a
+// tag no later visit has): a stored wait was computed from exactly the
+// moments its tag names.
+#define PU_LDS_Q 3400u                     // queues of the LDS header image (a 32x32 mesh has 1,984)
+#define PU_LDS_SLOT 2u                     // 16-B pieces per LDS header slot
 #define PU_MG1_CACHE_NONE 0xFFFFFFFFFFFFFFFFull
 #define PU_MG1_WAIT_BITS 32
 #define AS3 __attribute__((address_space(3)))
-static __shared__ v4u32 lds_qhdr[PU_LDS_QHDR_BYTES / 16];
+static __shared__ v4u32 lds_qhdr[PU_LDS_Q * PU_LDS_SLOT];
+static __shared__ uint64_t lds_qcache[PU_LDS_Q];
 // queue ids whose header the main wave just wrote back, for the helper
 #define PU_HQ 256u
 static __shared__ uint16_t lds_hq[PU_HQ];
 static __shared__ uint32_t lds_hq_head;    // ids pushed so far (main writes)
 static __shared__ uint32_t lds_main_done;  // the main wave left its request loop
 
-// Header write-back of queue q by the calling lane(s): pieces a = {n, Σs} and
-// b = {Σs², newest} (every visit changes them: one aligned 32-B half line),
-// and c = {head, count, f0} only when the visit changed the free-interval
-// ring (a tree visit or its prune).
-template <bool LH>
+constexpr uint64_t PU_HDR_NMASK = (1ull << 48) - 1;
+constexpr double PU_TWO53 = 9007199254740992.0;
+__device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+// an integer below 2^53 as a double: two exact u32 conversions and one exact fma
+__device__ __forceinline__ double dbl48(uint64_t v) {
+    return __builtin_fma((double)(uint32_t)(v >> 32), 4294967296.0, (double)(uint32_t)v);
+}
+
+// Header write-back of queue q by the calling lane(s).  Packed: b = {newest,
+// f0} then a = {n0|head, n1|count} (one aligned 32-B piece pair).  Wide: a =
+// {n, Σs} and b = {Σs², newest} (every visit changes them), c = {head, count,
+// f0} only when the visit changed the free-interval ring.
+template <bool LH, bool WIDE>
 __device__ __forceinline__ void q_store_hdr(const NetCtx& c, int q, const QState& st, bool ring_changed = true) {
-    uint64_t sb = (uint64_t)__double_as_longlong(st.sum), qb = (uint64_t)__double_as_longlong(st.sum_sq);
-    const uint64_t nb = (uint64_t)__double_as_longlong(st.n);
-    const v4u32 a = v4u32{(uint32_t)nb, (uint32_t)(nb >> 32), (uint32_t)sb, (uint32_t)(sb >> 32)};
-    const v4u32 b = v4u32{(uint32_t)qb, (uint32_t)(qb >> 32), (uint32_t)st.newest, (uint32_t)(st.newest >> 32)};
-    const v4u32 cc = v4u32{st.head, st.count, (uint32_t)st.f0, (uint32_t)(st.f0 >> 32)};
-    if constexpr (LH) {
-        // b and c first, a (with n) last: see the M/G/1 cache above
-        volatile AS3 v4u32* H = (volatile AS3 v4u32*)&lds_qhdr[(size_t)q * PU_LDS_SLOT];
-        H[1] = b;
-        if (ring_changed) H[2] = cc;
-        H[0] = a;
-    } else {
+    if constexpr (WIDE) {
+        uint64_t sb = (uint64_t)__double_as_longlong(st.sum), qb = (uint64_t)__double_as_longlong(st.sum_sq);
+        const uint64_t nb = (uint64_t)__double_as_longlong(st.n);
+        const v4u32 a = v4u32{(uint32_t)nb, (uint32_t)(nb >> 32), (uint32_t)sb, (uint32_t)(sb >> 32)};
+        const v4u32 b = v4u32{(uint32_t)qb, (uint32_t)(qb >> 32), (uint32_t)st.newest, (uint32_t)(st.newest >> 32)};
+        const v4u32 cc = v4u32{st.head, st.count, (uint32_t)st.f0, (uint32_t)(st.f0 >> 32)};
         AS1 v4u32* H = q_hdr_ab(c, q);
         H[0] = a;
         H[1] = b;
         if (ring_changed) *q_hdr_c(c, q) = cc;
+    } else {
+        const uint64_t w0 = st.n0 | ((uint64_t)st.head << 48), w1 = st.n1 | ((uint64_t)st.count << 48);
+        const v4u32 a = v4u32{(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
+        const v4u32 b = v4u32{(uint32_t)st.newest, (uint32_t)(st.newest >> 32), (uint32_t)st.f0,
+                              (uint32_t)(st.f0 >> 32)};
+        if constexpr (LH) {
+            // b first, a (with n) last: see the M/G/1 cache above
+            volatile AS3 v4u32* H = (volatile AS3 v4u32*)&lds_qhdr[(size_t)q * PU_LDS_SLOT];
+            H[1] = b;
+            H[0] = a;
+        } else {
+            AS1 v4u32* H = reinterpret_cast<AS1 v4u32*>(c.qhdr + (uint64_t)q * PU_HDR_BYTES);
+            H[0] = a;
+            H[1] = b;
+        }
     }
 }
 
 // M/G/1 update (queue_model_m_g_1.cpp:45-55) and header write-back (lane 0).
-template <bool LH>
+template <bool LH, bool WIDE>
 __device__ __forceinline__ void q_finish(const NetCtx& c, int q, QState& st, uint64_t t, uint64_t p, uint64_t d) {
-    st.sum_sq = st.sum_sq + (double)p * (double)p;
-    st.sum = st.sum + (double)p;
-    st.n = st.n + 1.0;
+    if constexpr (WIDE) {
+        st.sum_sq = st.sum_sq + (double)p * (double)p;
+        st.sum = st.sum + (double)p;
+        st.n = st.n + 1.0;
+    } else {
+        if (p == c.p0) st.n0++;
+        else st.n1++;
+    }
     uint64_t fin = t + d + p;
     st.newest = fin > st.newest ? fin : st.newest;
-    if (lane_id() == 0) q_store_hdr<LH>(c, q, st);
+    if (lane_id() == 0) q_store_hdr<LH, WIDE>(c, q, st);
 }
 
 // One computeQueueDelay on a uniform header (bus queues, unit tests).
-template <bool LH>
+template <bool LH, bool WIDE>
 __device__ __forceinline__ uint64_t q_step(const NetCtx& c, int q, QState& st, uint64_t t, uint64_t p, uint64_t minp,
                                            uint64_t& mg1, uint64_t& err) {
     uint64_t d;
@@ -742,46 +791,73 @@ __device__ __forceinline__ uint64_t q_step(const NetCtx& c, int q, QState& st, u
             st.f0 = f1;
         }
     }
-    q_finish<LH>(c, q, st, t, p, d);
+    if constexpr (!WIDE)
+        if (p != c.p0 && p != c.p1) err |= PU_ERRF_QUEUE;   // a length the packed header cannot count
+    q_finish<LH, WIDE>(c, q, st, t, p, d);
     return d;
 }
 
-__device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
-__device__ __forceinline__ QState hdr_state(v4u32 a, v4u32 b, v4u32 c) {
+// The queue state a header holds.  Packed: the moments from the counts
+// (exact, see above; a moment at 2^53 or more sets PU_ERRF_QUEUE through
+// `err`).  Wide: as stored.
+template <bool WIDE>
+__device__ __forceinline__ QState hdr_state(const NetCtx& ctx, v4u32 a, v4u32 b, v4u32 c, uint64_t& err) {
     QState st;
-    st.n = __longlong_as_double((long long)u64of(a.x, a.y));
-    st.sum = __longlong_as_double((long long)u64of(a.z, a.w));
-    st.sum_sq = __longlong_as_double((long long)u64of(b.x, b.y));
-    st.newest = u64of(b.z, b.w);
-    st.head = c.x;
-    st.count = c.y;
-    st.f0 = u64of(c.z, c.w);
+    if constexpr (WIDE) {
+        st.n = __longlong_as_double((long long)u64of(a.x, a.y));
+        st.sum = __longlong_as_double((long long)u64of(a.z, a.w));
+        st.sum_sq = __longlong_as_double((long long)u64of(b.x, b.y));
+        st.newest = u64of(b.z, b.w);
+        st.head = c.x;
+        st.count = c.y;
+        st.f0 = u64of(c.z, c.w);
+        st.n0 = st.n1 = 0;
+    } else {
+        const uint64_t w0 = u64of(a.x, a.y), w1 = u64of(a.z, a.w);
+        st.n0 = w0 & PU_HDR_NMASK;
+        st.n1 = w1 & PU_HDR_NMASK;
+        st.head = (uint32_t)(w0 >> 48);
+        st.count = (uint32_t)(w1 >> 48);
+        st.newest = u64of(b.x, b.y);
+        st.f0 = u64of(b.z, b.w);
+        const double d0 = dbl48(st.n0), d1 = dbl48(st.n1);
+        const double p0 = (double)ctx.p0, p1 = (double)ctx.p1;
+        st.n = d0 + d1;
+        st.sum = __builtin_fma(p1, d1, p0 * d0);
+        st.sum_sq = __builtin_fma(p1 * p1, d1, (p0 * p0) * d0);
+        if (st.sum_sq >= PU_TWO53) err |= PU_ERRF_QUEUE;
+    }
     return st;
 }
 __device__ __forceinline__ v4u32 uni4(v4u32 v) { return v4u32{uni32(v.x), uni32(v.y), uni32(v.z), uni32(v.w)}; }
-template <bool LH>
+template <bool LH, bool WIDE>
 __device__ __forceinline__ void hdr_load(const NetCtx& c, int q, v4u32& a, v4u32& b, v4u32& cc) {
-    if constexpr (LH) {
-        const AS3 v4u32* H = (const AS3 v4u32*)&lds_qhdr[(size_t)q * PU_LDS_SLOT];
-        a = H[0];
-        b = H[1];
-        cc = H[2];
-    } else {
+    if constexpr (WIDE) {
         const AS1 v4u32* H = q_hdr_ab(c, q);
         a = H[0];
         b = H[1];
         cc = *q_hdr_c(c, q);
+    } else if constexpr (LH) {
+        const AS3 v4u32* H = (const AS3 v4u32*)&lds_qhdr[(size_t)q * PU_LDS_SLOT];
+        a = H[0];
+        b = H[1];
+        cc = v4u32{0u, 0u, 0u, 0u};
+    } else {
+        const AS1 v4u32* H = reinterpret_cast<const AS1 v4u32*>(c.qhdr + (uint64_t)q * PU_HDR_BYTES);
+        a = H[0];
+        b = H[1];
+        cc = v4u32{0u, 0u, 0u, 0u};
     }
 }
 
 // A whole queue op loading its own state (bus queues, unit tests).
-template <bool LH>
+template <bool LH, bool WIDE>
 __device__ __forceinline__ uint64_t q_op(const NetCtx& c, int q, uint64_t t, uint64_t p, uint64_t minp, uint64_t& mg1,
                                          uint64_t& err) {
     v4u32 a, b, cc;
-    hdr_load<LH>(c, q, a, b, cc);
-    QState st = hdr_state(uni4(a), uni4(b), uni4(cc));
-    return q_step<LH>(c, q, st, t, p, minp, mg1, err);
+    hdr_load<LH, WIDE>(c, q, a, b, cc);
+    QState st = hdr_state<WIDE>(c, uni4(a), uni4(b), uni4(cc), err);
+    return q_step<LH, WIDE>(c, q, st, t, p, minp, mg1, err);
 }
 
 // n / d for n < 2^16 as a multiply-high by m = ceil(2^32 / d) (exact there:
@@ -910,7 +986,7 @@ static __shared__ uint32_t lds_dir_w[2][32];
 // branches.  The protocol code reaches it from four sites only.
 // Lane h prefetches hop h's link header and the two interval starts at its
 // ring head; only hops taking the tree branch fetch their full ring.
-template <bool LH, int NL>
+template <bool LH, int NL, bool WIDE>
 __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char* base_in, int src, int dst, int len,
                                                  uint64_t timer, uint32_t& hq_head) {
     PROF_T(p_pre);
@@ -919,6 +995,8 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
     c.qhdr = base + OFF(g->off_qhdr);
     c.qring = base + OFF(g->off_qring);
     c.hdr_c = (uint32_t)g->nqueues * PU_HDR_AB;
+    c.p0 = (uint32_t)g->header_flits;     // packed headers: 0-byte messages ...
+    c.p1 = (uint32_t)g->plen_blk;         // ... and blocks
     c.router = (uint32_t)g->router_delay;
     c.link_delay = (uint32_t)g->link_delay;
     c.inject = (uint32_t)g->inject_delay;
@@ -937,23 +1015,28 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
     timer = uni64(timer);
     if (src == dst) return 0;
     const int ln = lane_id();
-    // network.cpp:104 packet length; the engine only sends 0-byte and block messages
+    // network.cpp:104 packet length; the engine only sends 0-byte and block
+    // messages (the packed header counts those two lengths; the unit hook's
+    // wide header takes any)
     const int plen = len == 0 ? c.header_flits
                    : len == c.blk_len ? c.plen_blk
                    : c.header_flits + (int)ceil((double)len / (double)c.data_width);
+    uint64_t err = 0;
+    if constexpr (!WIDE)
+        if (len != 0 && len != c.blk_len) err |= PU_ERRF_QUEUE;
     int sx, sy, sz, rx, ry, rz;
     net_coords(c, src, sx, sy, sz);
     net_coords(c, dst, rx, ry, rz);
     const int hx = abs(rx - sx), hy = abs(ry - sy), hz = abs(rz - sz);
     const int hops = hx + hy + hz;
     uint64_t t = timer + c.inject;
-    uint64_t mg1 = 0, err = 0;
+    uint64_t mg1 = 0;
     PROF_ADD(PF_NPRE, p_pre);
     for (int b0 = 0; b0 < hops; b0 += 64) {
         PROF_T(p_setup);
         PROF_CNT(PF_WINDOWS, 1);
         // ---- prefetch the window: lane h = hop b0+h loads its link's header
-        // (48 B: moments, ring cursor, the first interval start)
+        // (32 B: visit counts, ring cursor, newest finish, the first interval start)
         const int h = b0 + ln;
         const int nh = hops - b0 < 64 ? hops - b0 : 64;
         int rq = 0;
@@ -961,8 +1044,8 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         uint64_t vcache = PU_MG1_CACHE_NONE;
         if (h < hops) {
             rq = net_route_link(c, h, sx, sy, sz, rx, ry, rz, hx, hy);
-            hdr_load<LH>(c, rq, ha, hb, hc);
-            if constexpr (LH) vcache = *(const AS3 uint64_t*)&lds_qhdr[(size_t)rq * PU_LDS_SLOT + 3];
+            hdr_load<LH, WIDE>(c, rq, ha, hb, hc);
+            if constexpr (LH) vcache = lds_qcache[rq];
         }
         // Everything about hop h that does not depend on its arrival time is
         // computed by lane h here, once per window: the front interval (the
@@ -970,7 +1053,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         // from the pre-update moments (queue_model_m_g_1.cpp:16-42) and the
         // moment updates of q_finish.  The route's links are distinct, so no
         // hop sees another hop's update.
-        const QState hs = hdr_state(ha, hb, hc);
+        const QState hs = hdr_state<WIDE>(c, ha, hb, hc, err);
         uint32_t vhead = hs.head, vcnt = hs.count;
         uint64_t vf0 = hs.f0;
         const uint64_t vfront = vf0;    // the tree's minimum: the M/G/1 test
@@ -1190,11 +1273,17 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
             st.head = vhead;
             st.count = vcnt;
             st.f0 = vf0;
-            st.sum_sq = st.sum_sq + (double)plen * (double)plen;
-            st.sum = st.sum + (double)plen;
-            st.n = st.n + 1.0;
+            if constexpr (WIDE) {
+                st.sum_sq = st.sum_sq + (double)plen * (double)plen;
+                st.sum = st.sum + (double)plen;
+                st.n = st.n + 1.0;
+            } else if (plen == (int)c.p0) {
+                st.n0++;
+            } else {
+                st.n1++;
+            }
             st.newest = vfin > st.newest ? vfin : st.newest;
-            q_store_hdr<LH>(c, rq, st, vhead != hs.head || vcnt != hs.count || vf0 != hs.f0);
+            q_store_hdr<LH, WIDE>(c, rq, st, vhead != hs.head || vcnt != hs.count || vf0 != hs.f0);
             if constexpr (LH) lds_hq[(hq_head + (uint32_t)ln) & (PU_HQ - 1)] = (uint16_t)rq;
         }
         if constexpr (LH) {   // publish the window's links to the helper, after their ids
@@ -1325,14 +1414,17 @@ __device__ void mg1_helper(const Geo* __restrict__ g, const char* base, const pu
             const v4u32 b = H[1];
             asm volatile("" ::: "memory");
             const v4u32 a2 = H[0];
-            const QState st = hdr_state(a, b, v4u32{0u, 0u, 0u, 0u});   // M/G/1 needs a and b only
+            NetCtx hc;                      // the helper only sees link queues: 0-byte and block packets
+            hc.p0 = (uint32_t)g->header_flits;
+            hc.p1 = (uint32_t)g->plen_blk;
+            uint64_t herr = 0;
+            const QState st = hdr_state<false>(hc, a, b, v4u32{0u, 0u, 0u, 0u}, herr);
             const uint64_t w = mg1_wait(st);
             const uint64_t wmask = (1ull << PU_MG1_WAIT_BITS) - 1;
             const bool same = a.x == a2.x && a.y == a2.y && a.z == a2.z && a.w == a2.w;
-            const bool st_ok = same && w < wmask && st.n < 4294967296.0;
+            const bool st_ok = same && !herr && w < wmask && st.n < 4294967296.0;
             if (st_ok)
-                *(volatile AS3 uint64_t*)&lds_qhdr[(size_t)q * PU_LDS_SLOT + 3] =
-                    w | ((uint64_t)((uint32_t)st.n ^ (uint32_t)w) << PU_MG1_WAIT_BITS);
+                *(volatile AS3 uint64_t*)&lds_qcache[q] = w | ((uint64_t)((uint32_t)st.n ^ (uint32_t)w) << PU_MG1_WAIT_BITS);
 #ifdef PU_PROF
             const uint64_t nst = __builtin_popcountll(ballot(st_ok));
             if (ln == 0) atomicAdd(&lds_prof[PF_MG1STORED], (unsigned long long)nst);
@@ -1343,7 +1435,7 @@ __device__ void mg1_helper(const Geo* __restrict__ g, const char* base, const pu
     }
 }
 
-template <int NL, bool LH = false>
+template <int NL, bool LH = false, bool WIDE = false>
 struct Engine {
     const Geo* __restrict__ g;
     char* base;
@@ -1373,6 +1465,7 @@ struct Engine {
         c.qhdr = (AS1 char*)base + OFF(g->off_qhdr);
         c.qring = (AS1 char*)base + OFF(g->off_qring);
         c.hdr_c = (uint32_t)g->nqueues * PU_HDR_AB;
+        c.p0 = c.p1 = (uint32_t)g->bus_latency;   // packed headers: a bus queue sees one packet length
         c.router = (uint32_t)g->router_delay;
         c.link_delay = (uint32_t)g->link_delay;
         c.inject = (uint32_t)g->inject_delay;
@@ -1384,7 +1477,7 @@ struct Engine {
     }
     __device__ __forceinline__ uint64_t transmit(int src, int dst, int len, uint64_t timer) {
         PROF_T(p0);
-        uint64_t d = net_transmit<LH, NL>(g, base, src, dst, len, timer, hq_head);
+        uint64_t d = net_transmit<LH, NL, WIDE>(g, base, src, dst, len, timer, hq_head);
         PROF_ADD(PF_NET, p0);
         return d;
     }
@@ -2054,7 +2147,7 @@ struct Engine {
         if (L.has_bus) {              // Bus::access (bus.cpp:55-61)
             stat_add(SN_BUSACC, 1);
             uint64_t bl = (uint64_t)g->bus_latency, mg1 = 0, err = 0;
-            int db = (int)q_op<LH>(net_ctx(), L.bus_q0 + cid, (uint64_t)(timer + dly), bl, bl, mg1, err);
+            int db = (int)q_op<LH, WIDE>(net_ctx(), L.bus_q0 + cid, (uint64_t)(timer + dly), bl, bl, mg1, err);
             stat_add(SN_MG1, mg1);
             if (err) err_or(err);
             stat_add(SN_BUSCONT, (uint64_t)(int64_t)db);
@@ -2227,7 +2320,7 @@ struct Engine {
         if (L.has_bus) {              // Bus::access (bus.cpp:55-61)
             stat_add(SN_BUSACC, 1);
             uint64_t bl = (uint64_t)g->bus_latency, mg1 = 0, err = 0;
-            int db = (int)q_op<LH>(net_ctx(), L.bus_q0 + cid, (uint64_t)(timer + dly), bl, bl, mg1, err);
+            int db = (int)q_op<LH, WIDE>(net_ctx(), L.bus_q0 + cid, (uint64_t)(timer + dly), bl, bl, mg1, err);
             stat_add(SN_MG1, mg1);
             if (err) err_or(err);
             stat_add(SN_BUSCONT, (uint64_t)(int64_t)db);
@@ -2453,28 +2546,18 @@ __device__ __forceinline__ int pool_next(uint32_t* sched, int cur) {
     return r < (int)uni32((uint32_t)lds_pool.nrep) ? r : -1;
 }
 
-// Latency mode: the replica's queue headers (HBM lines of PU_HDR_PIECES
-// 16-B pieces) into / out of the LDS image (PU_LDS_SLOT pieces per queue:
-// a, b, c and the M/G/1 cache word d, which starts empty).  Thread t of the
-// two-wave workgroup copies slots t, t + 128, ...
+// Latency mode: the replica's packed queue headers (32 B each, the same
+// layout in HBM and in the LDS image) into / out of the LDS image, and the
+// M/G/1 cache words set empty.  Thread t of the two-wave workgroup copies
+// pieces t, t + 128, ...
 __device__ __forceinline__ void hdr_image_in(const char* qhdr, uint32_t nqueues, uint32_t t) {
     const AS1 v4u32* gh = (const AS1 v4u32*)(AS1 char*)qhdr;
-    const AS1 v4u32* gc = gh + (size_t)nqueues * (PU_HDR_AB / 16);
-    const uint32_t nq4 = nqueues * PU_LDS_SLOT;
-    for (uint32_t k = t; k < nq4; k += 128) {
-        const uint32_t q = k >> 2, p = k & 3u;
-        lds_qhdr[k] = p < 2u ? gh[q * 2 + p] : p == 2u ? gc[q] : v4u32{~0u, ~0u, 0u, 0u};
-    }
+    for (uint32_t k = t; k < nqueues * PU_LDS_SLOT; k += 128) lds_qhdr[k] = gh[k];
+    for (uint32_t k = t; k < nqueues; k += 128) lds_qcache[k] = PU_MG1_CACHE_NONE;
 }
 __device__ __forceinline__ void hdr_image_out(char* qhdr, uint32_t nqueues, uint32_t t) {
     AS1 v4u32* gh = (AS1 v4u32*)(AS1 char*)qhdr;
-    AS1 v4u32* gc = gh + (size_t)nqueues * (PU_HDR_AB / 16);
-    const uint32_t nq4 = nqueues * PU_LDS_SLOT;
-    for (uint32_t k = t; k < nq4; k += 128) {
-        const uint32_t q = k >> 2, p = k & 3u;
-        if (p < 2u) gh[q * 2 + p] = lds_qhdr[k];
-        else if (p == 2u) gc[q] = lds_qhdr[k];
-    }
+    for (uint32_t k = t; k < nqueues * PU_LDS_SLOT; k += 128) gh[k] = lds_qhdr[k];
 }
 
 // One replica's message loop (prime.cpp:120-137): reqs[b .. end) in order, D
@@ -2770,20 +2853,30 @@ namespace {
 #ifndef PU_JIT_GEO
 // Queue records start as the single free interval [0, UINT64_MAX]
 // (QueueModelHistoryTree ctor, queue_model_history_tree.cpp:28).
+// Packed headers (the engine): n0 = n1 = 0, head 0, count 1, newest 0, f0 0;
+// wide headers (the unit hooks): n, Σs, Σs², newest 0, then head 0, count 1, f0 0.
 __global__ void init_queues_kernel(char* arena, uint64_t replica_bytes, uint64_t off_qhdr, uint64_t off_qring,
-                                   int nqueues, int nreplicas) {
+                                   int nqueues, int nreplicas, int wide) {
     uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t total = (uint64_t)nqueues * (uint64_t)nreplicas;
     if (id >= total) return;
     uint64_t r = id / (uint64_t)nqueues, q = id % (uint64_t)nqueues;
     char* base = arena + r * replica_bytes;
-    uint64_t* ab = reinterpret_cast<uint64_t*>(base + off_qhdr + q * PU_HDR_AB);
-    for (int i = 0; i < 4; i++) ab[i] = 0;   // n, sum, sum_sq, newest
-    uint32_t* cc = reinterpret_cast<uint32_t*>(base + off_qhdr + (uint64_t)nqueues * PU_HDR_AB + q * PU_HDR_C);
-    cc[0] = 0;   // head
-    cc[1] = 1;   // count
-    cc[2] = 0;   // f0
-    cc[3] = 0;
+    if (wide) {
+        uint64_t* ab = reinterpret_cast<uint64_t*>(base + off_qhdr + q * PU_HDR_AB);
+        for (int i = 0; i < 4; i++) ab[i] = 0;   // n, sum, sum_sq, newest
+        uint32_t* cc = reinterpret_cast<uint32_t*>(base + off_qhdr + (uint64_t)nqueues * PU_HDR_AB + q * PU_HDR_C);
+        cc[0] = 0;   // head
+        cc[1] = 1;   // count
+        cc[2] = 0;   // f0
+        cc[3] = 0;
+    } else {
+        uint64_t* h = reinterpret_cast<uint64_t*>(base + off_qhdr + q * PU_HDR_BYTES);
+        h[0] = 0;                 // n0 | head << 48
+        h[1] = 1ull << 48;        // n1 | count << 48
+        h[2] = 0;                 // newest
+        h[3] = 0;                 // f0
+    }
     QueueSlot* ring = reinterpret_cast<QueueSlot*>(base + off_qring) + q * PU_QRING;
     ring[0] = QueueSlot{0ull, UINT64_MAX};
 }
@@ -2793,7 +2886,7 @@ __global__ __launch_bounds__(64) void unit_queue_kernel(const Geo* __restrict__ 
                                                         const uint64_t* __restrict__ t,
                                                         const uint64_t* __restrict__ p, uint64_t n,
                                                         uint64_t* __restrict__ out, uint64_t* __restrict__ mg1) {
-    Engine<1> e;
+    Engine<1, false, true> e;   // wide headers: any packet length
     e.g = g;
     e.ln = lane_id();
     e.base = base;
@@ -2801,7 +2894,7 @@ __global__ __launch_bounds__(64) void unit_queue_kernel(const Geo* __restrict__ 
     const NetCtx c = e.net_ctx();
     uint64_t calls = 0, err = 0;
     for (uint64_t i = 0; i < n; i++) {
-        uint64_t d = q_op<false>(c, 0, t[i], p[i], minp, calls, err);
+        uint64_t d = q_op<false, true>(c, 0, t[i], p[i], minp, calls, err);
         if (e.ln == 0) out[i] = d;
     }
     if (e.ln == 0) *mg1 = calls;
@@ -2813,7 +2906,7 @@ __global__ __launch_bounds__(64) void unit_network_kernel(const Geo* __restrict_
                                                           const int32_t* __restrict__ len,
                                                           const uint64_t* __restrict__ timer, uint64_t n,
                                                           uint64_t* __restrict__ out) {
-    Engine<1> e;
+    Engine<1, false, true> e;   // wide headers: any packet length
     e.g = g;
     e.ln = lane_id();
     e.base = base;
@@ -2958,15 +3051,15 @@ extern "C" int pu_engine_occupancy(int num_levels, int mode, int* blocks_per_cu,
 }
 
 // Queue headers of one replica that fit the latency-mode LDS image.
-extern "C" int pu_engine_lds_header_queues(void) { return PU_LDS_QHDR_BYTES / (16 * PU_LDS_SLOT); }   // 64-B slots
+extern "C" int pu_engine_lds_header_queues(void) { return (int)PU_LDS_Q; }
 
 extern "C" int pu_engine_init_queues(char* arena, uint64_t replica_bytes, uint64_t off_qhdr, uint64_t off_qring,
-                                     int nqueues, int nreplicas, hipStream_t stream) {
+                                     int nqueues, int nreplicas, int wide, hipStream_t stream) {
     uint64_t total = (uint64_t)nqueues * (uint64_t)nreplicas;
     if (total == 0) return 0;
     unsigned blocks = (unsigned)((total + 255) / 256);
     hipLaunchKernelGGL(init_queues_kernel, dim3(blocks), dim3(256), 0, stream, arena, replica_bytes, off_qhdr,
-                       off_qring, nqueues, nreplicas);
+                       off_qring, nqueues, nreplicas, wide);
     return hipGetLastError() == hipSuccess ? 0 : PU_EIO;
 }
 

@@ -19,9 +19,10 @@
 //     pool     : pool_entries x nwords x u64 bitmaps + a free stack
 //     dalive, dcnt : per slice
 //   queues (Graphite history tree restated as a ring of sorted free intervals):
-//     qhdr : nqueues x QueueHdr (48 B in a 64-B line: M/G/1 moments, ring cursor
-//            and the first interval start, so the M/G/1-vs-tree decision of a
-//            hop needs the header only)  — links first, then per-cache buses
+//     qhdr : nqueues x 32-B packed header (visit counts of the two packet
+//            lengths -> the M/G/1 moments, ring cursor, newest finish, the
+//            first interval start, so the M/G/1-vs-tree decision of a hop
+//            needs the header only; engine.hip)  — links first, then buses
 //     qring: nqueues x 128 x {first,second} (2 KB)
 //   dram : banks x DramBank (opt-in bank model, pu_dram_cfg; absent when off)
 //   stats (EngineStats), per-core completion cycles, run state.
@@ -78,20 +79,21 @@ struct DirLine {
 #define PU_SH_POOL 0xFF
 #define PU_DIR_PROG_ESC 1023u
 
-// 48 B (three 16-B pieces): the prune of a full history (size >= 100 at the
-// start of computeQueueDelay, queue_model_history_tree.cpp:49-55) is applied
-// eagerly at the end of the tree op that fills it — nothing observes the tree
-// in between, and an M/G/1 visit never grows it — so the header needs the
-// tree's minimum (the M/G/1 test) but not the one after it.
-// Three 16-B pieces: a = {n, Σs} and b = {Σs², newest} change on every visit
-// (an M/G/1 visit writes back one aligned 32-B half line), c = {head, count,
-// f0} only when the visit edits the free-interval ring.
-// In HBM the pieces are two arrays: {a, b} of every queue (32 B each, an
-// M/G/1 visit's read-modify-write of one aligned 32-B piece pair), then c of
-// every queue (16 B each): the consecutive queues of a route segment share
-// 128-B lines four (a, b) or eight (c) at a time.
-constexpr uint32_t PU_HDR_AB = 32, PU_HDR_C = 16;
-constexpr uint32_t PU_HDR_BYTES = PU_HDR_AB + PU_HDR_C;   // per queue
+// The prune of a full history (size >= 100 at the start of
+// computeQueueDelay, queue_model_history_tree.cpp:49-55) is applied eagerly at
+// the end of the tree op that fills it — nothing observes the tree in
+// between, and an M/G/1 visit never grows it — so the header needs the tree's
+// minimum (the M/G/1 test) but not the one after it.
+// The engine's packed header is 32 B: a = {n0 | head << 48, n1 | count << 48}
+// (visit counts of the two packet lengths a queue sees, ring cursor), b =
+// {newest, f0}; every visit rewrites it (one aligned 32-B read-modify-write),
+// and the consecutive queues of a route segment share a 128-B line four at a
+// time (engine.hip explains the exact moments).  The unit hooks' wide header
+// (any packet length) is 48 B as two arrays: {a, b} of every queue (a = {n,
+// Σs}, b = {Σs², newest}, 32 B), then c of every queue ({head, count, f0}, 16 B).
+constexpr uint32_t PU_HDR_BYTES = 32;                      // per queue, the engine
+constexpr uint32_t PU_HDR_AB = 32, PU_HDR_C = 16;          // wide header pieces (unit hooks)
+constexpr uint32_t PU_HDR_WIDE_BYTES = PU_HDR_AB + PU_HDR_C;
 
 struct QueueSlot {
     uint64_t first;

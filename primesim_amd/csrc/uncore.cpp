@@ -48,7 +48,7 @@ extern "C" int pu_engine_unit_network(const Geo* d_geo, char* base, const int32_
                                       const int32_t* len, const uint64_t* timer, uint64_t n, uint64_t* out,
                                       hipStream_t s);
 extern "C" int pu_engine_init_queues(char* arena, uint64_t replica_bytes, uint64_t off_qhdr, uint64_t off_qring,
-                                     int nqueues, int nreplicas, hipStream_t stream);
+                                     int nqueues, int nreplicas, int wide, hipStream_t stream);
 extern "C" int pu_engine_occupancy(int num_levels, int mode, int* blocks_per_cu, int* lds_bytes);
 
 namespace pu {
@@ -337,7 +337,7 @@ int reset_state(pu_handle* h) {
     HIP_TRY(hipMemset2DAsync(h->arena + h->geo.off_completion, h->geo.replica_bytes, 0xFF,
                              (size_t)h->geo.num_cores * 8, (size_t)h->R, h->stream), PU_EIO);
     int rc = pu_engine_init_queues(h->arena, h->geo.replica_bytes, h->geo.off_qhdr, h->geo.off_qring,
-                                   h->geo.nqueues, h->R, h->stream);
+                                   h->geo.nqueues, h->R, 0, h->stream);
     if (rc) return pu::set_error(rc, "queue init launch failed");
     rc = pu_engine_init_pool(h->arena, h->geo.replica_bytes, h->geo.dir.off_pool_free, h->geo.off_run,
                              h->geo.dir.pool_entries, h->R, h->stream);
@@ -1228,7 +1228,7 @@ int pu_unit_queue_run(uint64_t min_proc, const uint64_t* t, const uint64_t* p, s
     uint64_t* dmg = b.up<uint64_t>(nullptr, 1);
     if (!dg || !base || !dt || !dp || !dout || !dmg) return pu::set_error(PU_ENOMEM, "unit buffers");
     HIP_TRY(hipMemset(base, 0, g.replica_bytes), PU_EIO);
-    rc = pu_engine_init_queues(base, g.replica_bytes, g.off_qhdr, g.off_qring, 1, 1, nullptr);
+    rc = pu_engine_init_queues(base, g.replica_bytes, g.off_qhdr, g.off_qring, 1, 1, 1, nullptr);   // wide header
     if (rc) return pu::set_error(rc, "queue init failed");
     rc = pu_engine_unit_queue(dg, base, min_proc, dt, dp, n, dout, dmg, nullptr);
     if (rc) return pu::set_error(rc, "unit queue launch failed");
@@ -1286,7 +1286,7 @@ int pu_unit_network_run(int num_nodes, int net_type, int data_width, int header_
     g.nlinks = w > 1 ? (w - 1) * w * (net_type == 1 ? 3 * w : 2) : 0;
     g.nqueues = g.nlinks;
     Layout lay;
-    g.off_qhdr = lay.take((uint64_t)g.nqueues * PU_HDR_BYTES);
+    g.off_qhdr = lay.take((uint64_t)g.nqueues * PU_HDR_WIDE_BYTES);   // the unit hook's wide headers
     g.off_qring = lay.take((uint64_t)g.nqueues * PU_QRING * sizeof(QueueSlot));
     g.off_stats = lay.take(sizeof(EngineStats));
     g.replica_bytes = align_up(lay.cur, 4096);
@@ -1300,7 +1300,7 @@ int pu_unit_network_run(int num_nodes, int net_type, int data_width, int header_
     uint64_t* dout = b.up<uint64_t>(nullptr, n);
     if (!dg || !base || !ds || !dd || !dl || !dt || !dout) return pu::set_error(PU_ENOMEM, "unit buffers");
     HIP_TRY(hipMemset(base, 0, g.replica_bytes), PU_EIO);
-    rc = pu_engine_init_queues(base, g.replica_bytes, g.off_qhdr, g.off_qring, g.nqueues, 1, nullptr);
+    rc = pu_engine_init_queues(base, g.replica_bytes, g.off_qhdr, g.off_qring, g.nqueues, 1, 1, nullptr);
     if (rc) return pu::set_error(rc, "queue init failed");
     rc = pu_engine_unit_network(dg, base, ds, dd, dl, dt, n, dout, nullptr);
     if (rc) return pu::set_error(rc, "unit network launch failed");

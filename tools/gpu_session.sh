@@ -25,6 +25,7 @@
 #                alone open / closed loop
 #   ab_single:V1,V2,...  the same, one simulation alone only
 #   ab_ens:V1,V2,...     the same, headline only (3 rounds)
+#   refwrap      tools/ref_overhead.py: the reference CPU uncore with and without the golden counting wraps
 #   residency    tools/probe/residency: one-wave workgroups resident per CU by resource shape
 #   diag:V       one headline run (5+5 steps) of variant V (ab syntax) with its bench log kept
 #   ab_pool      headline with the replica pool (--spare-replicas 0.1) vs without (0), 3 interleaved rounds
@@ -83,6 +84,7 @@ for S in "$@"; do
       timeout -k 10 200 python tools/prof_regions.py --jit -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras --replay closed > ${O}_regions_single_closed.txt 2>&1 || exit 1;;
     regions_ens)
       timeout -k 10 300 python tools/prof_regions.py --jit -- --steps 3 --warmup 5 --no-cpu --no-extras > ${O}_regions_ens.txt 2>&1 || exit 1;;
+    refwrap) timeout -k 10 200 python tools/ref_overhead.py --seconds 5 --rounds 3 --json ${O}_ref_overhead.json > ${O}_ref_overhead.log 2>&1 || exit 1;;
     residency) timeout -k 10 120 tools/probe/residency > ${O}_residency.json 2> ${O}_residency.log || exit 1;;
     diag:*) ( variant_env "${S#diag:}"
               timeout -k 10 300 $BENCH --steps 5 --warmup 5 --no-cpu --no-extras > ${O}_diag.json 2> ${O}_diag.log ) || exit 1;;

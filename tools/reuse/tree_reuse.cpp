@@ -3,7 +3,8 @@
 // plus a recorder of every link visit: which link, whether it took the tree
 // branch of computeQueueDelay (queue_model_history_tree.cpp:64-112, the
 // branch whose free-interval ring the lone wave stages and writes back), and
-// the history's size.  The recorder keeps the move-to-front stack of the
+// the index (from the front of the sorted free-interval list) of the
+// interval the tree search stopped at.  The recorder keeps the move-to-front stack of the
 // links that took the tree branch, so each tree visit's LRU stack distance
 // (distinct tree-visited links since its link's last tree visit) is known:
 // the hit rate an on-chip cache of the last K rings would have.
@@ -20,7 +21,8 @@ struct Rec {
     bool on = false;
     std::vector<uint32_t> mtf;                      // tree-visited links, most recent first
     uint64_t hist[kMaxDist + 1] = {};               // [d]: stack distance d; [kMaxDist]: beyond (or first)
-    uint64_t visits = 0, tree = 0, tree_ivs = 0;    // link visits, tree visits, summed ring sizes
+    uint64_t visits = 0, tree = 0, tree_ks = 0;     // link visits, tree visits, summed found indices
+    uint64_t khist[128] = {};                       // tree visits by found index
     uint64_t all_hist[kMaxDist + 1] = {};           // the same over every link visit
     std::vector<uint32_t> all_mtf;
 } g;
@@ -39,13 +41,14 @@ void mtf_push(std::vector<uint32_t>& s, uint64_t* hist, uint32_t link) {
 }
 }  // namespace
 
-void cpuref_trace_link(size_t link, bool tree, size_t intervals) {
+void cpuref_trace_link(size_t link, bool tree, size_t k) {
     if (!g.on) return;
     g.visits++;
     mtf_push(g.all_mtf, g.all_hist, (uint32_t)link);
     if (!tree) return;
     g.tree++;
-    g.tree_ivs += intervals;
+    g.tree_ks += k;
+    g.khist[k < 128 ? k : 127]++;
     mtf_push(g.mtf, g.hist, (uint32_t)link);
 }
 
@@ -56,19 +59,22 @@ void trace_enable(int on) {
     if (on) {
         for (auto& h : g.hist) h = 0;
         for (auto& h : g.all_hist) h = 0;
-        g.visits = g.tree = g.tree_ivs = 0;
+        g.visits = g.tree = g.tree_ks = 0;
+        for (auto& h : g.khist) h = 0;
     }
 }
-// out: [0] link visits, [1] tree visits, [2] summed ring sizes at tree visits,
-// then kMaxDist + 1 tree-visit stack-distance bins, then kMaxDist + 1 bins over all visits
+// out: [0] link visits, [1] tree visits, [2] summed found indices at tree visits,
+// then kMaxDist + 1 tree-visit stack-distance bins, then kMaxDist + 1 bins over
+// all visits, then 128 bins of tree visits by found index
 int trace_read(uint64_t* out, int n) {
-    const int need = 3 + 2 * (kMaxDist + 1);
+    const int need = 3 + 2 * (kMaxDist + 1) + 128;
     if (n < need) return -need;
     out[0] = g.visits;
     out[1] = g.tree;
-    out[2] = g.tree_ivs;
+    out[2] = g.tree_ks;
     for (int i = 0; i <= kMaxDist; i++) out[3 + i] = g.hist[i];
     for (int i = 0; i <= kMaxDist; i++) out[3 + kMaxDist + 1 + i] = g.all_hist[i];
+    for (int i = 0; i < 128; i++) out[3 + 2 * (kMaxDist + 1) + i] = g.khist[i];
     return need;
 }
 }

@@ -77,24 +77,28 @@ def main() -> None:
         if rc != 0:
             break
     L.trace_enable(0)
-    buf = np.zeros(3 + 2 * (KMAX + 1), dtype=np.uint64)
+    buf = np.zeros(3 + 2 * (KMAX + 1) + 128, dtype=np.uint64)
     assert L.trace_read(buf.ctypes.data, len(buf)) == len(buf)
-    visits, tree, ivs = int(buf[0]), int(buf[1]), int(buf[2])
+    visits, tree, ksum = int(buf[0]), int(buf[1]), int(buf[2])
     h_tree = buf[3:3 + KMAX + 1].astype(np.float64)
-    h_all = buf[3 + KMAX + 1:].astype(np.float64)
+    h_all = buf[3 + KMAX + 1:3 + 2 * (KMAX + 1)].astype(np.float64)
+    h_k = buf[3 + 2 * (KMAX + 1):].astype(np.float64)
     ks = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64, 128, 256, 512)
     res = {
         "replay": a.replay, "requests": done, "warmup_requests": n_w,
         "link_visits_per_access": visits / max(1, done),
         "tree_visits_per_access": tree / max(1, done),
-        "mean_ring_intervals_at_tree_visit": ivs / max(1, tree),
+        "mean_found_index_at_tree_visit": ksum / max(1, tree),
+        "tree_visits_found_below_k": {k: float(h_k[:k].sum() / max(1, tree)) for k in (1, 2, 4, 8, 16, 32, 64, 96, 128)},
         "tree_hit_rate_last_k_tree_rings": {k: float(h_tree[:k].sum() / max(1, tree)) for k in ks},
         "visit_hit_rate_last_k_links": {k: float(h_all[:k].sum() / max(1, visits)) for k in ks},
     }
     print(f"[tree_reuse] C4 replica 0, {a.replay} loop, {done} requests after a {n_w}-request warmup")
     print(f"  link visits/access {res['link_visits_per_access']:.1f}, tree visits/access "
-          f"{res['tree_visits_per_access']:.2f}, mean ring intervals at a tree visit "
-          f"{res['mean_ring_intervals_at_tree_visit']:.1f}")
+          f"{res['tree_visits_per_access']:.2f}, mean index of the interval a tree search stops at "
+          f"{res['mean_found_index_at_tree_visit']:.1f}")
+    print("  tree searches stopping below index K: " +
+          ", ".join(f"K={k} {v:.3f}" for k, v in res["tree_visits_found_below_k"].items()))
     print("  K    tree visits whose ring is among the last K tree-visited rings | any visit among the last K links")
     for k in ks:
         print(f"  {k:<4d} {res['tree_hit_rate_last_k_tree_rings'][k]:.3f}"
