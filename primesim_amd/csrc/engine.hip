@@ -150,14 +150,14 @@ struct RingView {
 // A queue's state as held by a lane (hdr_state): the ring cursor, the M/G/1
 // moments (queue_model_m_g_1.cpp: _num_arrivals as an exact double, the
 // service-time sum and sum of squares), the newest finish time, the first
-// free-interval start; n0 / n1 are the packed header's visit counts.
+// free-interval start; sum1 is the packed header's count of p1 visits.
 struct QState {
     uint32_t head, count;
     double n;           // _num_arrivals, held as an exact double (< 2^53)
     double sum, sum_sq;
     uint64_t newest;
     uint64_t f0;
-    uint64_t n0, n1;
+    double sum1;        // packed header: visits with packet length p1 (an exact double)
 };
 
 #define AS1 __attribute__((address_space(1)))
@@ -271,7 +271,7 @@ __device__ __forceinline__ void lds_or_u64_lane0(uint32_t lds_byte_addr, uint64_
 }
 // Device-scope atomic add by lane 0 (the per-cache counters), the same way.
 // Vector memory operations retire in issue order, so the compiler's vmcnt
-// waits (and vm_wait_dma's) stay correct with this one unseen: at worst they
+// waits (and the staging waits) stay correct with this one unseen: at worst they
 // wait for it too.
 __device__ __forceinline__ void gatomic_add_u64_lane0(uint64_t* p, uint64_t v) {
     uint64_t keep;
@@ -344,7 +344,7 @@ struct NetCtx {
     AS1 char* qring;           // ... and rings
     uint32_t router, link_delay, inject;
     uint32_t hdr_c;            // wide headers: byte offset of the c pieces (nqueues x 32)
-    uint32_t p0, p1;           // packed headers: the two packet lengths the visit counts n0, n1 stand for
+    uint32_t p0, p1;           // packed headers: the two packet lengths (n counts all visits, n1 those of p1)
     int header_flits, data_width, w, net_type;
     uint32_t w_magic, w2_magic;
     int w2, blk_len, plen_blk;
@@ -659,19 +659,21 @@ __device__ __forceinline__ uint64_t selm64(uint64_t m, uint64_t a, uint64_t b) {
 }
 // ---- queue headers ---------------------------------------------------------
 // The engine's header (PU_HDR_BYTES = 32 per queue, two 16-B pieces):
-//   a = {n0 | head << 48, n1 | count << 48}   b = {newest, f0}
-// n0 / n1 count the visits with packet length p0 / p1.  The engine sends only
-// two packet lengths over a link (0-byte messages: header_flits; blocks:
-// plen_blk, network.cpp:104) and one over a bus (bus_latency), so the M/G/1
-// moments of queue_model_m_g_1.cpp:45-55 follow from the counts:
-//   n = n0 + n1,  Σs = p0·n0 + p1·n1,  Σs² = p0²·n0 + p1²·n1
+//   a = {n | head, n1 | count}   b = {newest, f0}
+// n (all visits) and n1 (visits with packet length p1) are exact doubles; the
+// ring cursor rides in their low 7 mantissa bits, which are 0 for integers
+// below 2^45.  The engine sends only two packet lengths over a link (0-byte
+// messages: header_flits = p0; blocks: plen_blk = p1, network.cpp:104) and
+// one over a bus (bus_latency), so the M/G/1 moments of
+// queue_model_m_g_1.cpp:45-55 follow from the counts:
+//   Σs = p0·n + (p1 - p0)·n1,  Σs² = p0²·n + (p1² - p0²)·n1
 // — the same doubles the reference accumulates (each partial sum is an
-// integer below 2^53, so every addition is exact; a moment reaching 2^53 sets
-// PU_ERRF_QUEUE, an engine limit past ~10^14 visits of one link).  The ring
-// cursor (head, count) rides in the top bits of a, the first interval start
-// f0 (the M/G/1 test) in b: one 32-B read-modify-write per visit, four
-// neighbouring hops of a route per 128-B line (round 4's 48-B header read a
-// second line of c pieces per four hops).
+// integer below 2^53, so every addition is exact, and each fma's exact result
+// is representable; a moment reaching 2^53 or n reaching 2^45 sets
+// PU_ERRF_QUEUE, an engine limit past ~10^13 visits of one link).  The first
+// interval start f0 (the M/G/1 test) is in b: one 32-B read-modify-write per
+// visit, four neighbouring hops of a route per 128-B line (round 4's 48-B
+// header read a second line of c pieces per four hops).
 // The unit hooks (any packet length: unit_queue_kernel, unit_network_kernel)
 // keep the wide header (WIDE, PU_HDR_WIDE_BYTES = 48: {a, b} of every queue,
 // then c of every queue): a = {n, Σs}, b = {Σs², newest} as doubles,
@@ -714,16 +716,13 @@ static __shared__ uint16_t lds_hq[PU_HQ];
 static __shared__ uint32_t lds_hq_head;    // ids pushed so far (main writes)
 static __shared__ uint32_t lds_main_done;  // the main wave left its request loop
 
-constexpr uint64_t PU_HDR_NMASK = (1ull << 48) - 1;
-constexpr double PU_TWO53 = 9007199254740992.0;
+constexpr uint32_t PU_HDR_CUR = 0x7Fu;              // ring cursor bits in the low mantissa bits
+constexpr double PU_TWO53 = 9007199254740992.0, PU_TWO45 = 35184372088832.0;
 __device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
-// an integer below 2^53 as a double: two exact u32 conversions and one exact fma
-__device__ __forceinline__ double dbl48(uint64_t v) {
-    return __builtin_fma((double)(uint32_t)(v >> 32), 4294967296.0, (double)(uint32_t)v);
-}
+__device__ __forceinline__ double dbl_of(uint32_t lo, uint32_t hi) { return __longlong_as_double((long long)u64of(lo, hi)); }
 
 // Header write-back of queue q by the calling lane(s).  Packed: b = {newest,
-// f0} then a = {n0|head, n1|count} (one aligned 32-B piece pair).  Wide: a =
+// f0} then a = {n|head, n1|count} (one aligned 32-B piece pair).  Wide: a =
 // {n, Σs} and b = {Σs², newest} (every visit changes them), c = {head, count,
 // f0} only when the visit changed the free-interval ring.
 template <bool LH, bool WIDE>
@@ -739,8 +738,9 @@ __device__ __forceinline__ void q_store_hdr(const NetCtx& c, int q, const QState
         H[1] = b;
         if (ring_changed) *q_hdr_c(c, q) = cc;
     } else {
-        const uint64_t w0 = st.n0 | ((uint64_t)st.head << 48), w1 = st.n1 | ((uint64_t)st.count << 48);
-        const v4u32 a = v4u32{(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
+        const uint64_t w0 = (uint64_t)__double_as_longlong(st.n), w1 = (uint64_t)__double_as_longlong(st.sum1);
+        const v4u32 a = v4u32{(uint32_t)w0 | st.head, (uint32_t)(w0 >> 32), (uint32_t)w1 | st.count,
+                              (uint32_t)(w1 >> 32)};
         const v4u32 b = v4u32{(uint32_t)st.newest, (uint32_t)(st.newest >> 32), (uint32_t)st.f0,
                               (uint32_t)(st.f0 >> 32)};
         if constexpr (LH) {
@@ -764,8 +764,8 @@ __device__ __forceinline__ void q_finish(const NetCtx& c, int q, QState& st, uin
         st.sum = st.sum + (double)p;
         st.n = st.n + 1.0;
     } else {
-        if (p == c.p0) st.n0++;
-        else st.n1++;
+        st.n = st.n + 1.0;
+        if (p != c.p0) st.sum1 = st.sum1 + 1.0;
     }
     uint64_t fin = t + d + p;
     st.newest = fin > st.newest ? fin : st.newest;
@@ -811,21 +811,18 @@ __device__ __forceinline__ QState hdr_state(const NetCtx& ctx, v4u32 a, v4u32 b,
         st.head = c.x;
         st.count = c.y;
         st.f0 = u64of(c.z, c.w);
-        st.n0 = st.n1 = 0;
+        st.sum1 = 0.0;
     } else {
-        const uint64_t w0 = u64of(a.x, a.y), w1 = u64of(a.z, a.w);
-        st.n0 = w0 & PU_HDR_NMASK;
-        st.n1 = w1 & PU_HDR_NMASK;
-        st.head = (uint32_t)(w0 >> 48);
-        st.count = (uint32_t)(w1 >> 48);
+        st.head = a.x & PU_HDR_CUR;
+        st.count = a.z & PU_HDR_CUR;
+        st.n = dbl_of(a.x & ~PU_HDR_CUR, a.y);
+        st.sum1 = dbl_of(a.z & ~PU_HDR_CUR, a.w);
         st.newest = u64of(b.x, b.y);
         st.f0 = u64of(b.z, b.w);
-        const double d0 = dbl48(st.n0), d1 = dbl48(st.n1);
         const double p0 = (double)ctx.p0, p1 = (double)ctx.p1;
-        st.n = d0 + d1;
-        st.sum = __builtin_fma(p1, d1, p0 * d0);
-        st.sum_sq = __builtin_fma(p1 * p1, d1, (p0 * p0) * d0);
-        if (st.sum_sq >= PU_TWO53) err |= PU_ERRF_QUEUE;
+        st.sum = __builtin_fma(p1 - p0, st.sum1, p0 * st.n);
+        st.sum_sq = __builtin_fma(p1 * p1 - p0 * p0, st.sum1, (p0 * p0) * st.n);
+        if (st.sum_sq >= PU_TWO53 || st.n >= PU_TWO45) err |= PU_ERRF_QUEUE;
     }
     return st;
 }
@@ -935,19 +932,6 @@ __device__ __forceinline__ void ring_dma(const NetCtx& c, int q, uint32_t head, 
         : "=&s"(keep)
         : "v"(ga), "v"(gb), "s"(lo), "s"(hi)
         : "memory");
-}
-// Wait until at most `n` newer staging rings (2 DMAs each) are still in flight.
-__device__ __forceinline__ void vm_wait_dma(int n) {
-    switch (n) {
-        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-        case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-        case 6: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    }
 }
 __device__ __forceinline__ void ring_from_lds(int slot, RingView& v) {
     const int ln = lane_id();
@@ -1106,27 +1090,29 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         // its arrival + p — the first tree hop.  Hops before it are final; the
         // tree hop is done by the wave.  Its delay d replaces the assumed
         // M/G/1 wait, which moves every later arrival by the same d - wait:
-        // the latency mode (one wave alone, a dependent chain) carries that
-        // as one uniform shift `sh` (mod 2^64, like the sums); the throughput
-        // mode rescans after the tree hop (keeping the scan live across the
-        // tree operation costs registers there: -2.5% at 96 VGPRs, same-box).
+        // both kernels carry that as one uniform shift `sh` (mod 2^64, like
+        // the sums): one scan per window.  (Round 3 measured the throughput
+        // kernel 2.5% slower with the scan kept live across the tree
+        // operation at 96 VGPRs and had it rescan after each tree hop; with
+        // the 32-B headers that kernel spills no VGPR, and the shift is +0.5%
+        // on the C4 headline, same box: profiles/r5c_ab_ens.txt.)
         uint64_t S = 0, A0 = 0, sh = 0;
         const uint64_t t0 = t;
-        if constexpr (LH) {
+        {
             const uint64_t e = ln < nh ? vd + c.link_delay + c.router : 0;
             S = ballot(e >= (1ull << 26)) == 0 ? (uint64_t)scan_incl_u32((uint32_t)e) : scan_incl_u64(e);
             A0 = t + c.router + (S - e);
         }
         int js = 0;
-        if constexpr (LH) {
-            // latency kernel: the window's live hops and the M/G/1 hops'
-            // finish times as wave masks (one v_cndmask per dword), the
-            // staging slots as wrapping counters and a three-way DMA wait
-            // instead of a modulo and an eight-way ladder: one simulation
-            // alone +1.6% open loop, +3.4% closed loop (same-box A/B,
-            // profiles/r4d_ab_single.txt; a tree operation on wave masks,
-            // tree_op's predicates combined on the scalar unit, ran 9% slower
-            // closed loop: more scalar instructions than it saved)
+        {
+            // the window's live hops and the M/G/1 hops' finish times as wave
+            // masks (one v_cndmask per dword), the staging slots as wrapping
+            // counters and a three-way DMA wait instead of a modulo and an
+            // eight-way ladder: one simulation alone +1.6% open loop, +3.4%
+            // closed loop (same-box A/B, profiles/r4d_ab_single.txt; a tree
+            // operation on wave masks, tree_op's predicates combined on the
+            // scalar unit, ran 9% slower closed loop: more scalar
+            // instructions than it saved)
             const uint64_t nhm = nh >= 64 ? ~0ull : ((1ull << nh) - 1);
             int islot = issued % PU_RING_PF, cslot = 0;
             while (js < nh) {
@@ -1199,71 +1185,6 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                 PROF_ADD(PF_T_UPD, p_upd);          // prune, refill (T_REFILL), hop results into the window
                 PROF_ADD(PF_NTREE, p_tree);
             }
-        } else {
-        while (js < nh) {
-            const bool live = ln >= js && ln < nh;
-            uint64_t A;
-            if constexpr (LH) {
-                A = A0 + sh;
-            } else {
-                const uint64_t e = live ? vd + c.link_delay + c.router : 0;
-                // per-hop terms are small except past a saturated queue: a 32-bit
-                // scan then gives the same sums with a quarter of the VALU work
-                S = ballot(e >= (1ull << 26)) == 0 ? (uint64_t)scan_incl_u32((uint32_t)e) : scan_incl_u64(e);
-                A = t + c.router + (S - e);                   // arrival of hop ln (after its router)
-            }
-            const uint64_t cand = ballot(live && vfront <= A + (uint64_t)plen);
-            const int jt = cand ? (int)__builtin_ctzll(cand) : nh;
-            if (ln >= js && ln < jt) vfin = A + vd + (uint64_t)plen;
-            mg1 += (uint64_t)(jt - js);
-            if (jt == nh) {                                   // the rest of the window is M/G/1
-                t = LH ? t0 + rl64(S, nh - 1) + sh : t + rl64(S, nh - 1);
-                break;
-            }
-            PROF_T(p_tree);
-            PROF_CNT(PF_TREEHOPS, 1);
-            const uint64_t tj = rl64(A, jt);
-            const int q = (int)rl32((uint32_t)rq, jt);
-            uint32_t head = rl32(vhead, jt), cnt = rl32(vcnt, jt);
-            uint64_t f0n, f1n, d;
-            RingView v;
-            const bool staged = mc && jt == (int)__builtin_ctzll(mc);
-            if (staged) {
-                // predicted: its ring is (being) staged in LDS slot consumed % PF
-                mc &= mc - 1;
-                PROF_T(p_wait);
-                vm_wait_dma(issued - consumed - 1);
-                PROF_ADD(PF_NWAIT, p_wait);
-                ring_from_lds(consumed % PU_RING_PF, v);
-                consumed++;
-            } else {                            // not predicted (arrival pushed past the front)
-                PROF_CNT(PF_DEMAND, 1);
-                ring_load(c, q, head, cnt, v);
-            }
-            d = tree_op(c, q, v, head, cnt, tj, (uint64_t)plen, c.link_delay, err, f0n, f1n);
-            if (cnt >= PU_QMAX) {               // the next call's prune (history_tree.cpp:49-55), done now
-                head = (head + 1) & (PU_QRING - 1);
-                cnt--;
-                f0n = f1n;
-            }
-            if (staged && mi) {                 // keep PF rings in flight
-                PROF_T(p_r);
-                const int jj = (int)__builtin_ctzll(mi);
-                mi &= mi - 1;
-                ring_dma(c, (int)rl32((uint32_t)rq, jj), rl32(vhead, jj), rl32(vcnt, jj), issued % PU_RING_PF);
-                issued++;
-                PROF_ADD(PF_T_REFILL, p_r);
-            }
-            if constexpr (LH) sh += d - rl64(vd, jt);
-            vhead = wl32(vhead, head, jt);
-            vcnt = wl32(vcnt, cnt, jt);
-            vf0 = wl64(vf0, f0n, jt);
-            vd = wl64(vd, d, jt);
-            vfin = wl64(vfin, tj + d + (uint64_t)plen, jt);
-            t = tj + d + c.link_delay;
-            js = jt + 1;
-            PROF_ADD(PF_NTREE, p_tree);
-        }
         }
         PROF_ADD(PF_NHOPS, p_hops);
         PROF_T(p_wb);
@@ -1277,10 +1198,9 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                 st.sum_sq = st.sum_sq + (double)plen * (double)plen;
                 st.sum = st.sum + (double)plen;
                 st.n = st.n + 1.0;
-            } else if (plen == (int)c.p0) {
-                st.n0++;
             } else {
-                st.n1++;
+                st.n = st.n + 1.0;
+                if (plen != (int)c.p0) st.sum1 = st.sum1 + 1.0;
             }
             st.newest = vfin > st.newest ? vfin : st.newest;
             q_store_hdr<LH, WIDE>(c, rq, st, vhead != hs.head || vcnt != hs.count || vf0 != hs.f0);
@@ -2853,7 +2773,7 @@ namespace {
 #ifndef PU_JIT_GEO
 // Queue records start as the single free interval [0, UINT64_MAX]
 // (QueueModelHistoryTree ctor, queue_model_history_tree.cpp:28).
-// Packed headers (the engine): n0 = n1 = 0, head 0, count 1, newest 0, f0 0;
+// Packed headers (the engine): n = n1 = 0.0, head 0, count 1, newest 0, f0 0;
 // wide headers (the unit hooks): n, Σs, Σs², newest 0, then head 0, count 1, f0 0.
 __global__ void init_queues_kernel(char* arena, uint64_t replica_bytes, uint64_t off_qhdr, uint64_t off_qring,
                                    int nqueues, int nreplicas, int wide) {
@@ -2872,8 +2792,8 @@ __global__ void init_queues_kernel(char* arena, uint64_t replica_bytes, uint64_t
         cc[3] = 0;
     } else {
         uint64_t* h = reinterpret_cast<uint64_t*>(base + off_qhdr + q * PU_HDR_BYTES);
-        h[0] = 0;                 // n0 | head << 48
-        h[1] = 1ull << 48;        // n1 | count << 48
+        h[0] = 0;                 // n = 0.0 | head 0
+        h[1] = 1;                 // n1 = 0.0 | count 1
         h[2] = 0;                 // newest
         h[3] = 0;                 // f0
     }

@@ -84,8 +84,8 @@ struct DirLine {
 // the end of the tree op that fills it — nothing observes the tree in
 // between, and an M/G/1 visit never grows it — so the header needs the tree's
 // minimum (the M/G/1 test) but not the one after it.
-// The engine's packed header is 32 B: a = {n0 | head << 48, n1 | count << 48}
-// (visit counts of the two packet lengths a queue sees, ring cursor), b =
+// The engine's packed header is 32 B: a = {n | head, n1 | count}
+// (visit counts as exact doubles, the ring cursor in their low bits), b =
 // {newest, f0}; every visit rewrites it (one aligned 32-B read-modify-write),
 // and the consecutive queues of a route segment share a 128-B line four at a
 // time (engine.hip explains the exact moments).  The unit hooks' wide header
