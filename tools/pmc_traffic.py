@@ -135,6 +135,7 @@ def main():
         "fabric_read_bytes_per_access": read_b32 / accesses,
         "fabric_read_bytes_per_access_fetch_size": f_kb * 1024.0 / accesses,
         "fabric_write_bytes_per_access": w_kb * 1024.0 / accesses,
+        "atomic_dram_32b_units_per_access": wr32["TCC_EA0_WRREQ_ATOMIC_DRAM_32B_sum"] / accesses,
         "read_fetch_size_ratio": read_b32 / (f_kb * 1024.0) if f_kb else None,
         "alg_bytes_per_launch": bench_line["roofline"]["alg_bytes_per_launch"],
         "alg_bytes_per_access": bench_line["roofline"]["alg_bytes_per_launch"] / accesses,
