@@ -959,6 +959,12 @@ __device__ __forceinline__ uint32_t lds_addr(T* p) {
     return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)p;
 }
 
+// Throughput kernels: the junk word the request-stream prefetch lands in (replica_loop)
+#ifndef PU_REQ_PF
+#define PU_REQ_PF 0
+#endif
+static __shared__ uint32_t lds_req_junk;
+
 // The request's home directory set, staged before the request transmit (lane
 // w = way w: bytes 0-15 and the two dwords of the sharer word).  Up to 32 ways.
 static __shared__ v4u32 lds_dir_a[32];
@@ -2523,6 +2529,15 @@ __device__ __forceinline__ bool replica_loop(Engine<NL, LH>& e, const pu_req* __
         if (uni32((uint32_t)lds_ctl.halted)) break;   // the rest is zero-filled below
         PROF_T(p_loop);
         const pu_req q = reqs[i];
+        if constexpr (!LH && PU_REQ_PF > 0) {
+            // the request stream is read by scalar loads at the top of each
+            // request, its latency exposed; every fourth request lane 0 pulls
+            // the line PU_REQ_PF requests ahead toward the L2 (one LDS-DMA
+            // dword into a junk word: no register waits for it, and the
+            // request's own L1 set load, issued next, is waited for anyway)
+            if ((i & 3) == 0 && i + PU_REQ_PF < end && e.ln == 0)
+                lds_dma<false>((const AS1 char*)(const char*)(reqs + i + PU_REQ_PF), lds_addr(&lds_req_junk));
+        }
         const bool core_ok = q.core >= 0 && q.core < e.g->num_cores;
         const uint32_t fl = uni32(lds_ctl.flags);
         if (e.ln == 0) lds_ctl.cur = i;
