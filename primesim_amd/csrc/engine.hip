@@ -1008,12 +1008,16 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
     // network.cpp:104 packet length; the engine only sends 0-byte and block
     // messages (the packed header counts those two lengths; the unit hook's
     // wide header takes any)
-    const int plen = len == 0 ? c.header_flits
-                   : len == c.blk_len ? c.plen_blk
-                   : c.header_flits + (int)ceil((double)len / (double)c.data_width);
+    int plen;
     uint64_t err = 0;
-    if constexpr (!WIDE)
+    if constexpr (WIDE) {
+        plen = len == 0 ? c.header_flits
+             : len == c.blk_len ? c.plen_blk
+             : c.header_flits + (int)ceil((double)len / (double)c.data_width);
+    } else {
+        plen = len == 0 ? c.header_flits : c.plen_blk;
         if (len != 0 && len != c.blk_len) err |= PU_ERRF_QUEUE;
+    }
     int sx, sy, sz, rx, ry, rz;
     net_coords(c, src, sx, sy, sz);
     net_coords(c, dst, rx, ry, rz);
