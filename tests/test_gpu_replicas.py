@@ -136,14 +136,23 @@ def test_core_out_of_range():
         um.close()
 
 
-def test_any_prog_id_runs_exactly():
-    """Directory lines hold the whole int prog_id (InsMem::prog_id): large and
-    mixed program ids run exactly (the 0.1 engine packed 10 bits and stopped)."""
+@pytest.mark.parametrize("ids", ["large", "escape_edges", "negative"])
+def test_any_prog_id_runs_exactly(ids):
+    """Directory lines and packed L1 records keep the whole int prog_id
+    (InsMem::prog_id): ids outside the inline field (directory [0, 1023), L1
+    [0, 511)) escape to side arrays; large, negative and mixed ids around
+    both escape edges run exactly (the 0.1 engine packed 10 bits and stopped)."""
     cfg = P.config_from_dict(CF.preset("C1"))
     spec = P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 16, seed=23, max_requests=600)
     reqs = P.generate_stream(spec)
     hi = reqs.copy()
-    hi["prog_id"] = np.where(np.arange(len(hi)) % 3 == 0, 2**31 - 1, 1024 + (np.arange(len(hi)) % 5))
+    k = np.arange(len(hi))
+    if ids == "large":
+        hi["prog_id"] = np.where(k % 3 == 0, 2**31 - 1, 1024 + (k % 5))
+    elif ids == "escape_edges":
+        hi["prog_id"] = np.array([510, 511, 1022, 1023, 0, 2**31 - 1])[k % 6]
+    else:
+        hi["prog_id"] = np.where(k % 2 == 0, -1, -(2**31))
     um = P.UncoreManager()
     um.init(cfg)
     try:

@@ -37,8 +37,9 @@ O=gpurun_out/${T}
 BENCH="python bench.py"
 DRIVER="--steps 20 --warmup 5"
 
-variant_env() {   # V[#WAVES][@FLAGS]: library V (main = the product), compiled-configuration options
-  local v=$1 lib extra waves
+variant_env() {   # V[#WAVES][@FLAGS][^NAME=VALUE]: library V (main = the product), compiled-configuration
+  local v=$1 lib extra waves kv   # options, one more environment variable
+  case $v in *^*) kv=${v#*^}; v=${v%%^*}; export "${kv%%=*}=${kv#*=}";; esac
   lib=${v%%[@#]*}
   case $v in *@*) extra=${v#*@}; export PRIMEUNCORE_JIT_EXTRA="${extra//+/ }";; esac
   case $v in *#*) waves=${v#*#}; waves=${waves%%@*}; export PRIMEUNCORE_JIT_WAVES=$waves;; esac
