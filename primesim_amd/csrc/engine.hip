@@ -132,26 +132,6 @@ struct SetView {
     uint32_t w0;      // first way of the chunk held
 };
 
-// One cache level's line records as the set code reads and writes them.
-// Unpacked: LineMeta {tag, prog, state} and the int64 LRU timestamps, two
-// arrays.  Packed (LevelGeo.packed: the level's tags are below 2^52): one
-// 16-B record per line {word, ts} with word = tag | state << 52 | p9 << 55,
-// p9 the program id when 0 <= id < 511, else 511 and the full id in the side
-// array `prog` — a set probe reads one 128-B line for an 8-way set instead of
-// a line of LineMeta and half a line of timestamps.
-constexpr uint32_t PU_LINE_PROG_ESC = 511u;
-constexpr uint64_t PU_LINE_TAGMASK = (1ull << 52) - 1;
-struct SetArr {
-    char* meta;        // LineMeta[] or packed {word, ts} records
-    int64_t* ts;       // unpacked: timestamps
-    int32_t* prog;     // packed: program ids of escaped lines
-    bool pk;
-};
-__device__ __forceinline__ uint64_t pk_word(uint64_t tag, int32_t prog, uint32_t st) {
-    const uint32_t p9 = (uint32_t)prog < PU_LINE_PROG_ESC ? (uint32_t)prog : PU_LINE_PROG_ESC;
-    return tag | ((uint64_t)st << 52) | ((uint64_t)p9 << 55);
-}
-
 // Sets wider than 64 ways (walked in 64-way chunks, way order) are compiled
 // into configuration-specific kernels only (jit.cpp: the geometry is a
 // constant, so narrower configurations carry none of that code); pu_create
@@ -1306,7 +1286,7 @@ __device__ __forceinline__ void pf_requests(const Geo* __restrict__ g, const cha
         if (k == 0) p = (const char*)(reqs + first + j);
         else if (k <= 2) {
             if ((k - 1) * 64 < L.nways * sizeof(LineMeta)) p = base + L.off_meta + line0 * sizeof(LineMeta) + (k - 1) * 64;
-        } else if (k == 3 && !L.packed) p = base + L.off_ts + line0 * 8;   // packed records hold the timestamps
+        } else if (k == 3) p = base + L.off_ts + line0 * 8;
         else if (g->sys_type == 0 && k <= 6 && (k - 4) * 64 < g->dir.nways * sizeof(DirLine)) {
             const DirGeo& D = g->dir;
             int hb = (int)((addr >> g->home_offbits) & (((uint64_t)1 << g->home_mask_bits) - 1));
@@ -1427,37 +1407,26 @@ struct Engine {
     }
 
     // ------------------------------------------------------------ sets
-    // the line records of data-cache level l
-    __device__ __forceinline__ SetArr set_arr(const LevelGeo& L) const {
-        return SetArr{at<char>(OFF(L.off_meta)), at<int64_t>(OFF(L.off_ts)), at<int32_t>(OFF(L.off_prog)),
-                      L.packed != 0};
-    }
-    __device__ __forceinline__ void set_load(SetView& v, const SetArr& A, uint64_t nsets, uint64_t nways,
-                                             int offbits, int idxbits, uint64_t cache_index, uint64_t addr) const {
+    __device__ __forceinline__ void set_load(SetView& v, const LineMeta* meta, const int64_t* ts,
+                                             uint64_t nsets, uint64_t nways, int offbits, int idxbits,
+                                             uint64_t cache_index, uint64_t addr) const {
         v.set = set_index(addr, offbits, nsets);
         v.tag = addr >> (offbits + idxbits);
         // 32-bit index math: a level holds fewer than 2^32 lines (pu_create checks)
         v.line0 = (uint64_t)(((uint32_t)cache_index * (uint32_t)nsets + (uint32_t)v.set) * (uint32_t)nways);
-        set_chunk(v, A, nways, 0);
+        set_chunk(v, meta, ts, nways, 0);
     }
     // lane w <- way w0 + w of the set
-    __device__ __forceinline__ void set_chunk(SetView& v, const SetArr& A, uint64_t nways, uint32_t w0) const {
+    __device__ __forceinline__ void set_chunk(SetView& v, const LineMeta* meta, const int64_t* ts, uint64_t nways,
+                                              uint32_t w0) const {
         v.w0 = w0;
         const uint64_t w = (uint64_t)w0 + (uint64_t)ln;
-        if (w < nways && A.pk) {
-            const v2u64 rec = reinterpret_cast<const AS1 v2u64*>((AS1 char*)A.meta)[v.line0 + w];
-            v.mtag = rec.x & PU_LINE_TAGMASK;
-            v.mst = (uint32_t)(rec.x >> 52) & 7u;
-            const uint32_t p9 = (uint32_t)(rec.x >> 55);
-            v.mid = (int32_t)p9;
-            if (p9 == PU_LINE_PROG_ESC) v.mid = A.prog[v.line0 + w];
-            v.mts = (int64_t)rec.y;
-        } else if (w < nways) {
-            LineMeta m = reinterpret_cast<const LineMeta*>(A.meta)[v.line0 + w];
+        if (w < nways) {
+            LineMeta m = meta[v.line0 + w];
             v.mtag = m.tag;
             v.mid = m.id;
             v.mst = m.state;
-            v.mts = A.ts[v.line0 + w];
+            v.mts = ts[v.line0 + w];
         } else {
             v.mtag = 0;
             v.mid = 0;
@@ -1469,13 +1438,14 @@ struct Engine {
     // the lane holding `way` (a way of the chunk held)
     static __device__ __forceinline__ int wl(const SetView& v, int way) { return way - (int)v.w0; }
     // Cache::accessLine (cache.cpp:184-202): the first matching way
-    __device__ __forceinline__ int set_find(SetView& v, const SetArr& A, uint64_t nways, int prog) const {
+    __device__ __forceinline__ int set_find(SetView& v, const LineMeta* meta, const int64_t* ts, uint64_t nways,
+                                            int prog) const {
         if (!wide(nways)) {
             uint64_t m = ballot((uint64_t)ln < nways && v.mst != ST_I && v.mid == prog && v.mtag == v.tag);
             return m ? (int)__builtin_ctzll(m) : -1;
         }
         for (uint32_t c = 0;; c += 64) {
-            if (c != v.w0) set_chunk(v, A, nways, c);
+            if (c != v.w0) set_chunk(v, meta, ts, nways, c);
             const uint64_t m =
                 ballot((uint64_t)c + (uint64_t)ln < nways && v.mst != ST_I && v.mid == prog && v.mtag == v.tag);
             if (m) return (int)c + (int)__builtin_ctzll(m);
@@ -1484,8 +1454,9 @@ struct Engine {
     }
     // Cache::replaceLine (cache.cpp:204-235): first invalid way, else LRU
     // (strictly smaller timestamp, lowest way on ties).  Sets tag/id only.
-    __device__ __forceinline__ int set_replace(SetView& v, const SetArr& A, uint64_t nways, int offbits, int idxbits,
-                                               int prog, uint32_t* old_state, uint64_t* old_addr, int* old_prog) const {
+    __device__ __forceinline__ int set_replace(SetView& v, LineMeta* meta, const int64_t* ts, uint64_t nways,
+                                               int offbits, int idxbits, int prog, uint32_t* old_state,
+                                               uint64_t* old_addr, int* old_prog) const {
         int way = -1;
         bool invalid = false;
         if (!wide(nways)) {
@@ -1501,7 +1472,7 @@ struct Engine {
             // minimum over them: a later chunk wins only when strictly older
             int64_t best = INT64_MAX;
             for (uint32_t c = 0; (uint64_t)c < nways && !invalid; c += 64) {
-                if (c != v.w0) set_chunk(v, A, nways, c);
+                if (c != v.w0) set_chunk(v, meta, ts, nways, c);
                 const bool mine = (uint64_t)c + (uint64_t)ln < nways;
                 const uint64_t inv = ballot(mine && v.mst == ST_I);
                 if (inv) {
@@ -1516,7 +1487,7 @@ struct Engine {
                     }
                 }
             }
-            if ((uint32_t)way - v.w0 >= 64u) set_chunk(v, A, nways, (uint32_t)way & ~63u);
+            if ((uint32_t)way - v.w0 >= 64u) set_chunk(v, meta, ts, nways, (uint32_t)way & ~63u);
         }
         const int wlane = wl(v, way);
         if (invalid) {
@@ -1531,30 +1502,20 @@ struct Engine {
         if (ln == wlane) {
             v.mtag = v.tag;
             v.mid = prog;
-            const uint64_t line = v.line0 + (uint64_t)way;
-            if (A.pk) {
-                reinterpret_cast<uint64_t*>(A.meta)[2 * line] = pk_word(v.tag, prog, v.mst);
-                if ((uint32_t)prog >= PU_LINE_PROG_ESC) A.prog[line] = prog;
-            } else {
-                reinterpret_cast<LineMeta*>(A.meta)[line] = LineMeta{v.tag, prog, v.mst};
-            }
+            meta[v.line0 + (uint64_t)way] = LineMeta{v.tag, prog, v.mst};
         }
         return way;
     }
-    __device__ __forceinline__ void set_state(SetView& v, const SetArr& A, int way, uint32_t st) const {
+    __device__ __forceinline__ void set_state(SetView& v, LineMeta* meta, int way, uint32_t st) const {
         if (ln == wl(v, way)) {
             v.mst = st;
-            const uint64_t line = v.line0 + (uint64_t)way;
-            if (A.pk) reinterpret_cast<uint64_t*>(A.meta)[2 * line] = pk_word(v.mtag, v.mid, st);
-            else reinterpret_cast<LineMeta*>(A.meta)[line].state = st;
+            meta[v.line0 + (uint64_t)way].state = st;
         }
     }
-    __device__ __forceinline__ void set_ts(SetView& v, const SetArr& A, int way, int64_t t) const {
+    __device__ __forceinline__ void set_ts(SetView& v, int64_t* ts, int way, int64_t t) const {
         if (ln == wl(v, way)) {
             v.mts = t;
-            const uint64_t line = v.line0 + (uint64_t)way;
-            if (A.pk) reinterpret_cast<int64_t*>(A.meta)[2 * line + 1] = t;
-            else A.ts[line] = t;
+            ts[v.line0 + (uint64_t)way] = t;
         }
     }
 
@@ -1631,16 +1592,16 @@ struct Engine {
         const LevelGeo& L = g->lv[LV];
         uint32_t alive_v = ln == (cid & 63) ? at<uint32_t>(OFF(L.off_alive))[cid] : 0u;
         SetView v;
-        const SetArr A = set_arr(L);
-        set_load(v, A, L.nsets, L.nways, L.offbits, L.idxbits, (uint64_t)cid, r.addr);
+        set_load(v, at<LineMeta>(OFF(L.off_meta)), at<int64_t>(OFF(L.off_ts)), L.nsets, L.nways, L.offbits, L.idxbits,
+                 (uint64_t)cid, r.addr);
         if (!rl32(alive_v, cid & 63)) return 0;   // cache never created: NULL in the reference
         stat_add(SN_LOCKDOWN, 1);
         int d = L.access_time;
-        int way = set_find(v, A, L.nways, r.prog);
+        int way = set_find(v, at<LineMeta>(OFF(L.off_meta)), at<int64_t>(OFF(L.off_ts)), L.nways, r.prog);
         if (way >= 0) {
             uint32_t st = rl32(v.mst, wl(v, way));
             if (INVAL || st == ST_M || st == ST_E) {
-                set_state(v, A, way, INVAL ? ST_I : ST_S);
+                set_state(v, at<LineMeta>(OFF(L.off_meta)), way, INVAL ? ST_I : ST_S);
                 d += children<LV, INVAL>(cid, r);
             }
         }
@@ -2101,10 +2062,11 @@ struct Engine {
     __device__ __forceinline__ uint32_t mesi(int cid, const Req& r, int64_t timer) {
         const LevelGeo& L = g->lv[LV];
         constexpr bool kLast = LV == NL - 1;
-        const SetArr A = set_arr(L);
+        LineMeta* meta = at<LineMeta>(OFF(L.off_meta));
+        int64_t* tsa = at<int64_t>(OFF(L.off_ts));
         SetView v;
         PROF_T(p_set);
-        set_load(v, A, L.nsets, L.nways, L.offbits, L.idxbits, (uint64_t)cid, r.addr);
+        set_load(v, meta, tsa, L.nsets, L.nways, L.offbits, L.idxbits, (uint64_t)cid, r.addr);
         mark_alive(LV, cid);
         if (L.has_bus) {              // Bus::access (bus.cpp:55-61)
             stat_add(SN_BUSACC, 1);
@@ -2117,7 +2079,7 @@ struct Engine {
         }
         if (!hit) count<LV>(OFF(L.off_cnt), cid, 0);
         dly += L.access_time;
-        int way = set_find(v, A, L.nways, r.prog);
+        int way = set_find(v, meta, tsa, L.nways, r.prog);
         PROF_ADD(LV == 0 ? PF_SETL0 : PF_SETLN, p_set);
         bool is_miss = false, call_parent = false;
         int64_t ptimer = 0;
@@ -2128,13 +2090,13 @@ struct Engine {
         int wb_home = 0, req_reply = 0;
         Req wb_req = r;
         if (way >= 0) {                                      // hit
-            set_ts(v, A, way, timer + dly);
+            set_ts(v, tsa, way, timer + dly);
             hit = true;
             const uint32_t st = rl32(v.mst, wl(v, way));
             if (r.type == PU_WR) {
                 if constexpr (!kLast) {
                     if (st != ST_M) {
-                        set_state(v, A, way, ST_I);
+                        set_state(v, meta, way, ST_I);
                         call_parent = true;
                         ptimer = timer + dly;
                     }
@@ -2154,7 +2116,7 @@ struct Engine {
             uint32_t old_st;
             uint64_t old_addr;
             int old_prog;
-            way = set_replace(v, A, L.nways, L.offbits, L.idxbits, r.prog, &old_st, &old_addr, &old_prog);
+            way = set_replace(v, meta, tsa, L.nways, L.offbits, L.idxbits, r.prog, &old_st, &old_addr, &old_prog);
             if (old_st != ST_I) {
                 count<LV>(OFF(L.off_cnt), cid, 2);
                 Req o{old_addr, old_prog, PU_RD};
@@ -2168,7 +2130,7 @@ struct Engine {
                     }
                 }
             }
-            set_ts(v, A, way, timer + dly);
+            set_ts(v, tsa, way, timer + dly);
             if constexpr (!kLast) {
                 call_parent = true;
                 ptimer = timer;                               // `timer`, not timer+delay (Q2)
@@ -2181,7 +2143,7 @@ struct Engine {
             if (call_parent) {
                 const int parent = cid * L.share / g->lv[LV + 1].share;
                 const uint32_t ns = mesi<LV + 1>(parent, r, ptimer);
-                set_state(v, A, way, ns);
+                set_state(v, meta, way, ns);
                 if (is_miss) ret = ns;
             }
         } else {
@@ -2210,7 +2172,7 @@ struct Engine {
                 }
                 leg = wb ? (tx_req ? 1 : 3) : 2;
             }
-            set_state(v, A, way, is_miss ? ret : ST_M);
+            set_state(v, meta, way, is_miss ? ret : ST_M);
         }
         if (is_miss) count<LV>(OFF(L.off_cnt), cid, 1);
         return ret;
@@ -2235,8 +2197,7 @@ struct Engine {
     __device__ __forceinline__ bool snoop(int cid, const Req& r, int mode) {
         constexpr int last = NL - 1;
         const LevelGeo& L = g->lv[last];
-        const SetArr A = set_arr(L);
-        LineMeta* meta = reinterpret_cast<LineMeta*>(A.meta);
+        LineMeta* meta = at<LineMeta>(OFF(L.off_meta));
         const uint64_t set = set_index(r.addr, L.offbits, L.nsets);
         const uint64_t tag = r.addr >> (L.offbits + L.idxbits);
         bool any = false;
@@ -2245,26 +2206,12 @@ struct Engine {
             int myway = -1;
             uint32_t myst = ST_I;
             if (c < L.ncaches && c != cid) {
-                const uint64_t l0 = ((uint64_t)c * L.nsets + set) * L.nways;
+                const LineMeta* sp = meta + ((uint64_t)c * L.nsets + set) * L.nways;
                 for (uint64_t w = L.nways; w-- > 0;) {      // lowest matching way wins
-                    uint64_t mtag;
-                    int32_t mid;
-                    uint32_t mst;
-                    if (A.pk) {
-                        const uint64_t wd = reinterpret_cast<const uint64_t*>(A.meta)[2 * (l0 + w)];
-                        mtag = wd & PU_LINE_TAGMASK;
-                        mst = (uint32_t)(wd >> 52) & 7u;
-                        mid = (int32_t)(wd >> 55);
-                        if ((uint32_t)mid == PU_LINE_PROG_ESC) mid = A.prog[l0 + w];
-                    } else {
-                        const LineMeta m = meta[l0 + w];
-                        mtag = m.tag;
-                        mid = m.id;
-                        mst = m.state;
-                    }
-                    if (mst != ST_I && mid == r.prog && mtag == tag) {
+                    const LineMeta m = sp[w];
+                    if (m.state != ST_I && m.id == r.prog && m.tag == tag) {
                         myway = (int)w;
-                        myst = mst;
+                        myst = m.state;
                     }
                 }
             }
@@ -2278,16 +2225,7 @@ struct Engine {
                 any = true;
                 if (mode == 2) children<last, false>(i, r);
                 else children<last, true>(i, r);
-                if (ln == 0) {
-                    const uint64_t line = ((uint64_t)i * L.nsets + set) * L.nways + (uint64_t)way;
-                    const uint32_t ns = mode == 2 ? ST_S : ST_I;
-                    if (A.pk) {   // the holder's record, state field only
-                        uint64_t* wp = reinterpret_cast<uint64_t*>(A.meta) + 2 * line;
-                        *wp = (*wp & ~(7ull << 52)) | ((uint64_t)ns << 52);
-                    } else {
-                        meta[line].state = ns;
-                    }
-                }
+                if (ln == 0) meta[((uint64_t)i * L.nsets + set) * L.nways + (uint64_t)way].state = mode == 2 ? ST_S : ST_I;
                 if (mode != 0 && (st == ST_M || st == ST_E)) return any;
             }
         }
@@ -2298,9 +2236,10 @@ struct Engine {
     __device__ __forceinline__ uint32_t mesi_bus(int cid, const Req& r, int64_t timer) {
         const LevelGeo& L = g->lv[LV];
         constexpr bool kLast = LV == NL - 1;
-        const SetArr A = set_arr(L);
+        LineMeta* meta = at<LineMeta>(OFF(L.off_meta));
+        int64_t* tsa = at<int64_t>(OFF(L.off_ts));
         SetView v;
-        set_load(v, A, L.nsets, L.nways, L.offbits, L.idxbits, (uint64_t)cid, r.addr);
+        set_load(v, meta, tsa, L.nsets, L.nways, L.offbits, L.idxbits, (uint64_t)cid, r.addr);
         mark_alive(LV, cid);
         if (L.has_bus) {              // Bus::access (bus.cpp:55-61)
             stat_add(SN_BUSACC, 1);
@@ -2313,12 +2252,12 @@ struct Engine {
         }
         dly += L.access_time;
         if (!hit) count<LV>(OFF(L.off_cnt), cid, 0);
-        int way = set_find(v, A, L.nways, r.prog);
+        int way = set_find(v, meta, tsa, L.nways, r.prog);
         bool is_miss = false, call_parent = false;
         int snoop_mode = -1;
         uint32_t ret = ST_M;
         if (way >= 0) {                                      // hit
-            set_ts(v, A, way, timer + dly);
+            set_ts(v, tsa, way, timer + dly);
             hit = true;
             const uint32_t st = rl32(v.mst, wl(v, way));
             if (r.type != PU_WR) {
@@ -2327,7 +2266,7 @@ struct Engine {
             }
             if constexpr (!kLast) {
                 if (st != ST_M) {
-                    set_state(v, A, way, ST_I);
+                    set_state(v, meta, way, ST_I);
                     call_parent = true;
                 }
             } else {
@@ -2338,12 +2277,12 @@ struct Engine {
             uint32_t old_st;
             uint64_t old_addr;
             int old_prog;
-            way = set_replace(v, A, L.nways, L.offbits, L.idxbits, r.prog, &old_st, &old_addr, &old_prog);
+            way = set_replace(v, meta, tsa, L.nways, L.offbits, L.idxbits, r.prog, &old_st, &old_addr, &old_prog);
             if (old_st != ST_I) {
                 Req o{old_addr, old_prog, PU_RD};
                 children<LV, true>(cid, o);                  // inval_children, delay discarded
             }
-            set_ts(v, A, way, timer + dly);
+            set_ts(v, tsa, way, timer + dly);
             if constexpr (!kLast) call_parent = true;
             else snoop_mode = r.type == PU_WR ? 1 : 2;
         }
@@ -2351,7 +2290,7 @@ struct Engine {
             if (call_parent) {
                 const int parent = cid * L.share / g->lv[LV + 1].share;
                 const uint32_t ns = mesi_bus<LV + 1>(parent, r, timer + dly);   // timer + delay here
-                set_state(v, A, way, ns);
+                set_state(v, meta, way, ns);
                 if (is_miss) ret = ns;
             }
         } else {
@@ -2359,10 +2298,10 @@ struct Engine {
             if (snoop_mode >= 0) shared_line = snoop(cid, r, snoop_mode);
             if (is_miss) {
                 ret = r.type == PU_WR ? ST_M : (shared_line ? ST_S : ST_E);
-                set_state(v, A, way, ret);
+                set_state(v, meta, way, ret);
                 dly += dram(r.addr, timer + dly);
             } else {
-                set_state(v, A, way, ST_M);
+                set_state(v, meta, way, ST_M);
             }
         }
         if (is_miss) {
@@ -2417,23 +2356,24 @@ struct Engine {
     // request's address becomes physical (ppage << log2(page) | offset).
     __device__ __forceinline__ int tlb_translate(int core, Req& r, int64_t timer) {
         const TlbGeo& T = g->tlb;
-        const SetArr A{at<char>(OFF(T.off_meta)), at<int64_t>(OFF(T.off_ts)), nullptr, false};   // TLBs: unpacked
+        LineMeta* meta = at<LineMeta>(OFF(T.off_meta));
+        int64_t* tsa = at<int64_t>(OFF(T.off_ts));
         uint64_t* ppa = at<uint64_t>(OFF(T.off_ppage));
         SetView v;
-        set_load(v, A, T.nsets, T.nways, T.offbits, T.idxbits, (uint64_t)core, r.addr);
+        set_load(v, meta, tsa, T.nsets, T.nways, T.offbits, T.idxbits, (uint64_t)core, r.addr);
         const uint64_t mypp = !wide(T.nways) && (uint64_t)ln < T.nways ? ppa[v.line0 + (uint64_t)ln] : 0ull;
         count<PU_CNT_TLB>(OFF(T.off_cnt), core, 0);
         int d = T.access_time;
-        int way = set_find(v, A, T.nways, r.prog);
+        int way = set_find(v, meta, tsa, T.nways, r.prog);
         uint64_t ppage;
         if (way < 0) {
             uint32_t old_st;
             uint64_t old_addr;
             int old_prog;
-            way = set_replace(v, A, T.nways, T.offbits, T.idxbits, r.prog, &old_st, &old_addr, &old_prog);
+            way = set_replace(v, meta, tsa, T.nways, T.offbits, T.idxbits, r.prog, &old_st, &old_addr, &old_prog);
             if (old_st != ST_I) count<PU_CNT_TLB>(OFF(T.off_cnt), core, 2);
             count<PU_CNT_TLB>(OFF(T.off_cnt), core, 1);
-            set_state(v, A, way, ST_V);
+            set_state(v, meta, way, ST_V);
             ppage = page_translate(r.prog, r.addr >> T.offbits);
             if (ln == wl(v, way)) ppa[v.line0 + (uint64_t)way] = ppage;
             d += T.page_miss_delay;
@@ -2442,7 +2382,7 @@ struct Engine {
         } else {
             ppage = rl64(mypp, way);
         }
-        set_ts(v, A, way, timer);
+        set_ts(v, tsa, way, timer);
         r.addr = (ppage << T.offbits) | (r.addr % T.page_size);
         return d;
     }

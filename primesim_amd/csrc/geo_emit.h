@@ -46,7 +46,6 @@ inline std::string geo_cxx(const Geo& g, const char* var = "kJitGeo") {
         I32(offbits); I32(idxbits); I32(access_time); I32(share);
         I32(ncaches); I32(nchildren); I32(has_bus); I32(bus_q0);
         U64(off_meta); U64(off_ts); U64(off_alive); U64(off_cnt);
-        I32(packed); I32(_pad); U64(off_prog);
 #undef I32
 #undef U64
         o << "}, ";

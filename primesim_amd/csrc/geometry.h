@@ -7,8 +7,6 @@
 //   per data-cache level l (reference Cache, cache.h:102-164):
 //     meta[l]  : ncaches*nsets*nways x LineMeta (16 B: tag, prog id, state)
 //     ts[l]    : ncaches*nsets*nways x int64 LRU timestamps
-//                (packed levels: one 16-B record {tag|state|prog9, ts} per
-//                line instead, + an int32 side array of escaped program ids)
 //     alive[l] : ncaches x u32 (reference creates caches lazily, system.cpp:172)
 //     cnt[l]   : ncaches x 4 x u64 (ins, miss, evict, wb)
 //   directory / shared-LLC slices (one per network node):
@@ -130,12 +128,6 @@ struct LevelGeo {
     int32_t offbits, idxbits, access_time, share;
     int32_t ncaches, nchildren, has_bus, bus_q0;   // bus queue index of cache 0
     uint64_t off_meta, off_ts, off_alive, off_cnt;
-    // packed line records (the level's tags are below 2^52: offbits + idxbits
-    // >= 12): off_meta holds one 16-B {tag|state|prog9, ts} record per line,
-    // off_prog the int32 program ids of lines whose id is outside [0, 511)
-    // (engine.hip SetArr); off_ts unused
-    int32_t packed, _pad;
-    uint64_t off_prog;
 };
 
 // Only the sets some address can reach at a home are stored: the home id and

@@ -226,19 +226,8 @@ int build_geo(const pu_sim_cfg* c, Geo* g, uint64_t pool_cap = 0) {
         LevelGeo& L = g->lv[l];
         uint64_t lines = (uint64_t)L.ncaches * L.nsets * L.nways;
         if (lines >= (1ull << 32)) return pu::set_error(PU_ENOTSUP, "at most 2^32 lines per cache level");
-        // one 16-B record per line when every tag fits 52 bits (engine.hip SetArr);
-        // PRIMEUNCORE_PACKED_SETS=0 keeps the two arrays (tests, A/B runs)
-        const char* pe = std::getenv("PRIMEUNCORE_PACKED_SETS");
-        L.packed = L.offbits + L.idxbits >= 12 && !(pe && pe[0] == '0') ? 1 : 0;
-        if (L.packed) {
-            L.off_meta = lay.take(lines * 16);
-            L.off_ts = 0;
-            L.off_prog = lay.take(lines * sizeof(int32_t));
-        } else {
-            L.off_meta = lay.take(lines * sizeof(LineMeta));
-            L.off_ts = lay.take(lines * sizeof(int64_t));
-            L.off_prog = 0;
-        }
+        L.off_meta = lay.take(lines * sizeof(LineMeta));
+        L.off_ts = lay.take(lines * sizeof(int64_t));
         L.off_alive = lay.take((uint64_t)L.ncaches * 4);
         L.off_cnt = lay.take((uint64_t)L.ncaches * 32);
     }

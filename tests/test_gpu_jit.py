@@ -10,7 +10,6 @@ throughput launches (short batches, many replicas).  Here a spread of goldens
 loop, a full-size digest) also runs with the ahead-of-time kernels only
 (PRIMEUNCORE_JIT=0) and with the ahead-of-time kernels for the throughput
 launches (PRIMEUNCORE_JIT_THROUGHPUT=0), and every handle reports its variant.
-The same spread runs with the two-array line records (PRIMEUNCORE_PACKED_SETS=0).
 """
 import pytest
 
@@ -36,15 +35,6 @@ def test_ahead_of_time_throughput_launches_match_reference(name, monkeypatch):
 @pytest.mark.parametrize("name", CASES)
 def test_ahead_of_time_kernels_match_reference(name, monkeypatch):
     monkeypatch.setenv("PRIMEUNCORE_JIT", "0")
-    test_engine_reproduces_reference(name)
-
-
-@pytest.mark.parametrize("name", CASES + ["l1_tlb_128way", "bus_192way", "verbose_l2"])
-def test_two_array_line_records_match_reference(name, monkeypatch):
-    """PRIMEUNCORE_PACKED_SETS=0: every cache level keeps LineMeta and the
-    timestamps as two arrays (the layout of levels whose tags need more than
-    52 bits) instead of one 16-B record per line."""
-    monkeypatch.setenv("PRIMEUNCORE_PACKED_SETS", "0")
     test_engine_reproduces_reference(name)
 
 

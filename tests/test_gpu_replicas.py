@@ -138,10 +138,10 @@ def test_core_out_of_range():
 
 @pytest.mark.parametrize("ids", ["large", "escape_edges", "negative"])
 def test_any_prog_id_runs_exactly(ids):
-    """Directory lines and packed L1 records keep the whole int prog_id
-    (InsMem::prog_id): ids outside the inline field (directory [0, 1023), L1
-    [0, 511)) escape to side arrays; large, negative and mixed ids around
-    both escape edges run exactly (the 0.1 engine packed 10 bits and stopped)."""
+    """Directory lines keep the whole int prog_id (InsMem::prog_id): ids
+    outside the inline 10-bit field [0, 1023) escape to a side array; large,
+    negative and mixed ids around the escape edge run exactly (the 0.1 engine
+    packed 10 bits and stopped)."""
     cfg = P.config_from_dict(CF.preset("C1"))
     spec = P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 16, seed=23, max_requests=600)
     reqs = P.generate_stream(spec)
