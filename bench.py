@@ -75,8 +75,9 @@ LIMITER = ("dependent-load latency and instruction issue (profiles/r4n_sq.json: 
 REQ_BYTES = 32          # sizeof(pu_req)
 VARIANTS = {0: "ahead-of-time kernels (runtime geometry) for every launch",
             1: "ahead-of-time kernels for the replicas (throughput launches); the configuration compiled into "
-               "the kernel (hipRTC, jit.cpp) for one simulation alone (latency launches)",
-            2: "configuration compiled into the kernel (hipRTC, jit.cpp) for every launch"}
+               "the kernel (jit.cpp) for one simulation alone (latency launches)",
+            2: "configuration compiled into the kernel (jit.cpp) for every launch"}
+COMPILERS = {1: "hipRTC at run time", 2: "hipcc at build time"}
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 SEED_BASE = 4
 STAGE_GROUP = 256       # replicas whose requests the host generates per staging copy
@@ -607,6 +608,7 @@ class Device:
         self.stream = torch.cuda.Stream(self.dev)
         assert self.stream.cuda_stream != 0
         self.compiled = P.uncore.lib().pu_compiled_config(self.um._handle())   # 0, 1 or 2 (primeuncore.h)
+        self.compiler = P.uncore.lib().pu_compiled_compiler(self.um._handle())   # 0, 1 hipRTC, 2 hipcc
 
     def headline(self, args, rank: int, world: int, keep: list):
         import primesim_amd as P
@@ -823,7 +825,7 @@ def main(argv=None) -> None:
                 "mg1_share_of_link_visits": H.delta["mg1_calls"] / max(1, H.delta["net_distance"]),
                 "error_flags": H.errf & ~A.PU_ERRF_NEG_DELAY,
                 "engine_build": P.uncore.library_source_hash(),
-                "engine_variant": VARIANTS[D.compiled],
+                "engine_variant": VARIANTS[D.compiled] + (f" ({COMPILERS[D.compiler]})" if D.compiler else ""),
             },
             "per_simulation_accesses_per_s": value / tot_slots,
             "single_instance": single,

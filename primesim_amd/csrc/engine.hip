@@ -31,8 +31,8 @@
 #include <stdint.h>
 #endif
 
-#ifdef __HIPCC_RTC__
-#include "primeuncore.h"      // the same file, registered under this name by jit.cpp
+#if defined(__HIPCC_RTC__) || defined(PU_JIT_OFFLINE)
+#include "primeuncore.h"      // the same file, registered (hipRTC) or written (offline) under this name by jit.cpp
 #else
 #include "../../include/primeuncore.h"
 #endif
@@ -164,13 +164,31 @@ struct QState {
 #ifndef PU_RING_PF
 #define PU_RING_PF 3   // staged rings in flight per wave (6 KB LDS: 5 waves/SIMD fit the CU's 160 KB)
 #endif
+// The throughput kernels' own count.  The compiled one-level configuration
+// runs 6 waves per SIMD with 2 staged rings: 5,424 B of LDS per wave = five
+// 1,280-B units, 25 per CU, so all 24 waves reside (3 rings would be six
+// units, 21 per CU); +4.0% on the C4 headline against 5 waves with 3 rings,
+// same box (profiles/r5j_ab_ens.txt).
+#ifndef PU_RING_PF_TP
+#if defined(PU_JIT_GEO) && PU_JIT_NL == 1
+#define PU_RING_PF_TP 2
+#else
+#define PU_RING_PF_TP PU_RING_PF
+#endif
+#endif
+template <bool LH>
+constexpr int ring_pf() { return LH ? PU_RING_PF : PU_RING_PF_TP; }
 // Waves per SIMD the kernel is compiled for (the register budget: 5 waves =
 // 96 VGPRs).  The one-level engine fits 96 with a 5-VGPR spill (once the
 // pool/page-table state moved to LDS) and runs 2.9% faster at 5 resident
 // waves than at 4 (120 VGPRs, no spill; same-box A/B); the deeper hierarchies
 // would spill ~120 VGPRs at 128, so they keep the compiler's choice.
 #ifndef PU_WAVES_1LEVEL
+#if defined(PU_JIT_GEO)
+#define PU_WAVES_1LEVEL 6   // compiled configuration: 76 VGPRs, no spill (jit.cpp's options)
+#else
 #define PU_WAVES_1LEVEL 5
+#endif
 #endif
 #define PU_MIN_WAVES(NL) ((NL) == 1 ? PU_WAVES_1LEVEL : 1)
 // native vectors (not classes), so loads/stores through global-address-space
@@ -902,20 +920,27 @@ __device__ __forceinline__ int net_route_link(const NetCtx& c, int h, int sx, in
     return inx ? (sz * w + sy) * w1 + ax : iny ? blk + (sz * w + rx) * w1 + ay : 2 * blk + (ry * w + rx) * w1 + az;
 }
 
-// LDS staging ring for predicted tree hops: PU_RING_PF full link rings per wave
+// LDS staging ring for predicted tree hops: ring_pf<LH>() full link rings per wave
 // (one wave per workgroup), filled by global_load_lds_dwordx4 and consumed in
 // hop order behind a counted vmcnt (loads, stores and LDS-DMA retire in issue
 // order, MI355X_MICROARCH.md §waitcnt; hipcc would drain everything instead).
-static __shared__ v2u64 lds_ring[PU_RING_PF][PU_QRING];
+static __shared__ v2u64 lds_ring[PU_RING_PF][PU_QRING];        // latency kernel (LH)
+static __shared__ v2u64 lds_ring_tp[PU_RING_PF_TP][PU_QRING];  // throughput kernels
+template <bool LH>
+__device__ __forceinline__ v2u64* ring_slot(int slot) {
+    if constexpr (LH) return lds_ring[slot];
+    else return lds_ring_tp[slot];
+}
 
 // Stage ring q (live slots [head, head+cnt)) into LDS slot `slot`; dead slots
 // read the head slot instead (one shared line) and are never used.
+template <bool LH>
 __device__ __forceinline__ void ring_dma(const NetCtx& c, int q, uint32_t head, uint32_t cnt, int slot) {
     const int ln = lane_id();
     const AS1 v2u64* R = q_ring(c, q);
     const AS1 v2u64* ga = R + ((((uint32_t)ln - head) & (PU_QRING - 1)) < cnt ? (uint32_t)ln : head);
     const AS1 v2u64* gb = R + ((((uint32_t)ln + 64 - head) & (PU_QRING - 1)) < cnt ? (uint32_t)ln + 64 : head);
-    const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) v2u64*)&lds_ring[slot][0];
+    const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) v2u64*)ring_slot<LH>(slot);
     const uint32_t lo = __builtin_amdgcn_readfirstlane(la), hi = lo + 64 * sizeof(v2u64);
     unsigned keep;
     // lgkmcnt(0): the slot's previous ds_reads have returned before it is refilled
@@ -933,9 +958,11 @@ __device__ __forceinline__ void ring_dma(const NetCtx& c, int q, uint32_t head, 
         : "v"(ga), "v"(gb), "s"(lo), "s"(hi)
         : "memory");
 }
+template <bool LH>
 __device__ __forceinline__ void ring_from_lds(int slot, RingView& v) {
     const int ln = lane_id();
-    const v2u64 a = lds_ring[slot][ln], b = lds_ring[slot][ln + 64];
+    const v2u64* r = ring_slot<LH>(slot);
+    const v2u64 a = r[ln], b = r[ln + 64];
     v = RingView{a.x, a.y, b.x, b.y};
 }
 
@@ -1070,7 +1097,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         // Hop j arrives no earlier than LB_j = t + (j+1)*router + j*link_delay
         // (queue delays are >= 0).  A hop whose front free interval starts by
         // LB_j + p cannot take the M/G/1 branch, so its full ring is certainly
-        // needed: stage those rings now, PU_RING_PF ahead, in hop order.
+        // needed: stage those rings now, ring_pf<LH>() ahead, in hop order.
         bool pred = false;
         if (ln < nh) {
             const uint64_t lb = t + (uint64_t)(ln + 1) * c.router + (uint64_t)ln * c.link_delay;
@@ -1079,10 +1106,11 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         const uint64_t M = ballot(pred);
         uint64_t mi = M, mc = M;        // issue / consume cursors over the predicted hops
         int issued = 0, consumed = 0;
-        while (mi && issued < PU_RING_PF) {
+        constexpr int RPF = ring_pf<LH>();
+        while (mi && issued < RPF) {
             const int jj = (int)__builtin_ctzll(mi);
             mi &= mi - 1;
-            ring_dma(c, (int)rl32((uint32_t)rq, jj), rl32(vhead, jj), rl32(vcnt, jj), issued % PU_RING_PF);
+            ring_dma<LH>(c, (int)rl32((uint32_t)rq, jj), rl32(vhead, jj), rl32(vcnt, jj), issued % RPF);
             issued++;
         }
         PROF_ADD(PF_NSETUP, p_setup);
@@ -1118,7 +1146,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
             // scalar unit, ran 9% slower closed loop: more scalar
             // instructions than it saved)
             const uint64_t nhm = nh >= 64 ? ~0ull : ((1ull << nh) - 1);
-            int islot = issued % PU_RING_PF, cslot = 0;
+            int islot = issued % RPF, cslot = 0;
             while (js < nh) {
                 const uint64_t live = nhm & (~0ull << js);
                 const uint64_t A = A0 + sh;
@@ -1145,14 +1173,14 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                     // predicted: its ring is (being) staged in LDS slot cslot
                     mc &= mc - 1;
                     PROF_T(p_wait);
-                    const int newer = issued - consumed - 1;  // rings issued after this one, < PU_RING_PF
-                    static_assert(PU_RING_PF <= 3, "the three-way wait covers at most 2 newer staged rings");
+                    const int newer = issued - consumed - 1;  // rings issued after this one, < RPF
+                    static_assert(RPF <= 3, "the three-way wait covers at most 2 newer staged rings");
                     if (newer <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     else if (newer == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
                     else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
                     PROF_ADD(PF_NWAIT, p_wait);
-                    ring_from_lds(cslot, v);
-                    cslot = cslot == PU_RING_PF - 1 ? 0 : cslot + 1;
+                    ring_from_lds<LH>(cslot, v);
+                    cslot = cslot == RPF - 1 ? 0 : cslot + 1;
                     consumed++;
                 } else {                            // not predicted (arrival pushed past the front)
                     PROF_CNT(PF_DEMAND, 1);
@@ -1173,8 +1201,8 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                     PROF_T(p_r);
                     const int jj = (int)__builtin_ctzll(mi);
                     mi &= mi - 1;
-                    ring_dma(c, (int)rl32((uint32_t)rq, jj), rl32(vhead, jj), rl32(vcnt, jj), islot);
-                    islot = islot == PU_RING_PF - 1 ? 0 : islot + 1;
+                    ring_dma<LH>(c, (int)rl32((uint32_t)rq, jj), rl32(vhead, jj), rl32(vcnt, jj), islot);
+                    islot = islot == RPF - 1 ? 0 : islot + 1;
                     issued++;
                     PROF_ADD(PF_T_REFILL, p_r);
                 }
@@ -2766,11 +2794,18 @@ __global__ __launch_bounds__(LH ? 128 : 64) __attribute__((amdgpu_waves_per_eu(L
         uncore_body<PU_JIT_NL, S, H>(&kJitGeo, arena, replica0, reqs, off, delays, pos, budget_ticks, flags, sched,  \
                                      nrep);                                                                          \
     }
+// PU_JIT_PART 0: the throughput kernels (one wave per replica), 1: the
+// latency kernels (headers in LDS + the M/G/1 helper); jit.cpp compiles each
+// part with its own options.  Undefined: all five (offline tools).
+#if !defined(PU_JIT_PART) || PU_JIT_PART == 0
 PU_JIT_KERNEL(pu_jit_uncore_s0_h0, 0, false)
-PU_JIT_KERNEL(pu_jit_uncore_s0_h1, 0, true)
 PU_JIT_KERNEL(pu_jit_uncore_s1_h0, 1, false)
-PU_JIT_KERNEL(pu_jit_uncore_s1_h1, 1, true)
 PU_JIT_KERNEL(pu_jit_uncore_s2_h0, 2, false)
+#endif
+#if !defined(PU_JIT_PART) || PU_JIT_PART == 1
+PU_JIT_KERNEL(pu_jit_uncore_s0_h1, 0, true)
+PU_JIT_KERNEL(pu_jit_uncore_s1_h1, 1, true)
+#endif
 namespace {
 #endif
 
@@ -2883,7 +2918,7 @@ __global__ void init_pool_kernel(char* arena, uint64_t replica_bytes, uint64_t o
 #endif  // !PU_JIT_GEO
 }  // namespace
 
-#ifndef __HIPCC_RTC__
+#if !defined(__HIPCC_RTC__) && !defined(PU_JIT_OFFLINE)   // the library's host side
 extern "C" int pu_engine_init_pool(char* arena, uint64_t replica_bytes, uint64_t off_pool_free, uint64_t off_run,
                                    int pool_entries, int nreplicas, hipStream_t stream) {
     uint64_t total = (uint64_t)pool_entries * (uint64_t)nreplicas;
@@ -3013,4 +3048,4 @@ extern "C" int pu_engine_prof_blocks(unsigned long long* t0, unsigned long long*
     return n;
 }
 #endif
-#endif  // !__HIPCC_RTC__
+#endif  // !__HIPCC_RTC__ && !PU_JIT_OFFLINE

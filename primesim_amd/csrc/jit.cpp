@@ -5,10 +5,16 @@
 // once per configuration with every geometry value as a constant: the
 // configuration's Geo is written out as C++ (geo_emit.h), the engine's own
 // sources (embedded in this library at build time, tools/embed_src.py) are
-// compiled against it by hipRTC for gfx950, and the code object is loaded with
-// hipModuleLoadData.  Constant geometry removes the kernel's scalar loads of
-// its configuration and the scalar address arithmetic around them, the
-// largest part of the lone wave's issue and wait time.
+// compiled against it for gfx950, and the code object is loaded with
+// hipModuleLoadData.  Two compilers: at build time (jit_warm, a process that
+// has put nothing on the GPU) the ROCm driver hipcc in a child process; on a
+// cache miss at run time hipRTC in-process.  The same source and options give
+// different code: at C4 hipcc's throughput kernel needs 76 VGPRs and spills
+// none where hipRTC's needs 80 and spills 11, +4.6% on the headline, same box
+// (profiles/r5l_ab_ens.txt); so the cache prefers hipcc's object.  Constant
+// geometry removes the kernel's scalar loads of its configuration and the
+// scalar address arithmetic around them, the largest part of the lone wave's
+// issue and wait time.
 //
 // Code objects are cached on disk as <source tag>-<hash of (sources, geometry,
 // target arch, options)>.hsaco: PRIMEUNCORE_JIT_CACHE, else jit_cache/ next to
@@ -21,10 +27,15 @@
 // a load fails (with a message).  hipRTC itself is a link-time dependency of
 // the library (-lhiprtc), not an optional one.
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <spawn.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
 #include <utime.h>
 #include <unistd.h>
 
+#include <atomic>
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -44,6 +55,7 @@
 extern const int pu_jit_nsrc;
 extern const char* const pu_jit_src_name[];
 extern const char* const pu_jit_src_text[];
+extern char** environ;
 
 namespace pu {
 namespace {
@@ -105,7 +117,15 @@ void write_file_atomic(const std::string& path, const std::vector<char>& data) {
     if (std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
 }
 
-std::vector<std::string> options(const std::string& arch, int waves_1level) {
+// Part 0 (the throughput kernels) of a one-level configuration is compiled
+// without machine LICM: hoisted loop invariants (constants, address pairs)
+// were held in SGPRs across the whole request loop and spilled (192 spill
+// slots); rematerialised at their uses the kernel needs 76 VGPRs instead of 96
+// and fits 6 waves per SIMD with no spill.  6 waves + 2 staged rings + this:
+// +4.0% on the C4 headline (profiles/r5j_ab_ens.txt, r5k_ab_ens.txt); the
+// same flag at 5 waves lost 1.2%, and the latency kernels lost 1.5% open /
+// 2% closed loop with it (r5i_ab_nolicm.txt), so part 1 keeps the default.
+std::vector<std::string> options(const std::string& arch, int waves_1level, int part, bool one_level, int cc) {
     // max-occupancy: at C4 the throughput kernel spills 2 VGPRs instead of 4
     // and ran ahead of max-ILP in each of three interleaved rounds (233.0 /
     // 230.0 / 232.7 vs 215.9 / 226.9 / 231.4 M/s), one simulation alone level
@@ -117,6 +137,15 @@ std::vector<std::string> options(const std::string& arch, int waves_1level) {
                                   "-DPU_JIT_GEO=\"pu_jit_geo.h\"", "-Wno-c99-designator",
                                   "-Werror=missing-field-initializers"};
     if (waves_1level > 0) o.push_back("-DPU_WAVES_1LEVEL=" + std::to_string(waves_1level));
+    o.push_back("-DPU_JIT_PART=" + std::to_string(part));
+    if (cc == kJitOffline)   // the ROCm compiler driver: device code only, one code object, headers written flat
+        for (const char* x : {"-DPU_JIT_OFFLINE", "--cuda-device-only", "--no-gpu-bundle-output",
+                              "-Wno-unused-command-line-argument"})
+            o.push_back(x);
+    if (part == 0 && one_level) {
+        o.push_back("-mllvm");
+        o.push_back("-disable-machine-licm");
+    }
     // diagnostics only (tools/salu_lines.py: -gline-tables-only); the options
     // are part of the cache key, so such objects never stand in for the product's
     if (const char* e = std::getenv("PRIMEUNCORE_JIT_EXTRA"); e && *e) {
@@ -176,6 +205,86 @@ int compile(const std::string& geo_src, const std::vector<std::string>& opts, st
     return cs ? 0 : -1;
 }
 
+// The offline compiler (the ROCm driver, hipcc): PRIMEUNCORE_JIT_HIPCC, else
+// $ROCM_PATH/bin/hipcc; "0" turns it off.  Empty when absent.
+std::string offline_cc() {
+    const char* e = std::getenv("PRIMEUNCORE_JIT_HIPCC");
+    if (e && std::strcmp(e, "0") == 0) return "";
+    std::string p;
+    if (e && *e) {
+        p = e;
+    } else {
+        const char* r = std::getenv("ROCM_PATH");
+        p = std::string(r && *r ? r : "/opt/rocm") + "/bin/hipcc";
+    }
+    return ::access(p.c_str(), X_OK) == 0 ? p : "";
+}
+
+// Set once this process has loaded engine code on the GPU (jit_load): from
+// then on nothing is compiled by starting another program, only by hipRTC
+// in-process (a process that has initialised the GPU starts no compiler).
+std::atomic<bool> g_gpu_used{false};
+
+// Compile with the offline compiler (a child process, never from a process
+// that has initialised the GPU): the embedded sources and the configuration
+// are written to a scratch directory under the names the sources include.
+int compile_offline(const std::string& cc, const std::string& geo_src, const std::vector<std::string>& opts,
+                    std::vector<char>* code, std::string* log) {
+    const char* td = std::getenv("TMPDIR");
+    std::string tmpl = std::string(td && *td ? td : "/tmp") + "/pu_jit_XXXXXX";
+    std::vector<char> dbuf(tmpl.begin(), tmpl.end());
+    dbuf.push_back(0);
+    if (!::mkdtemp(dbuf.data())) {
+        *log = "mkdtemp failed";
+        return -1;
+    }
+    const std::string d = dbuf.data();
+    std::vector<std::string> files;
+    auto put = [&](const std::string& name, const char* text, size_t n) {
+        files.push_back(d + "/" + name);
+        std::ofstream f(files.back(), std::ios::binary);
+        f.write(text, (std::streamsize)n);
+        return (bool)f;
+    };
+    bool ok = true;
+    for (int i = 0; i < pu_jit_nsrc; i++)
+        ok = ok && put(pu_jit_src_name[i], pu_jit_src_text[i], std::strlen(pu_jit_src_text[i]));
+    ok = ok && put("pu_jit_geo.h", geo_src.data(), geo_src.size());
+    const std::string out = d + "/out.hsaco", logf = d + "/cc.log", src = d + "/engine.hip";
+    files.push_back(out);
+    files.push_back(logf);
+    int rc = -1;
+    if (ok) {
+        std::vector<std::string> args = {cc};
+        args.insert(args.end(), opts.begin(), opts.end());
+        for (const std::string& a : {std::string("-o"), out, std::string("-x"), std::string("hip"), src})
+            args.push_back(a);
+        std::vector<char*> argv;
+        for (auto& a : args) argv.push_back(&a[0]);
+        argv.push_back(nullptr);
+        posix_spawn_file_actions_t fa;
+        posix_spawn_file_actions_init(&fa);
+        posix_spawn_file_actions_addopen(&fa, 1, logf.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        posix_spawn_file_actions_adddup2(&fa, 1, 2);
+        pid_t pid = 0;
+        if (posix_spawn(&pid, cc.c_str(), &fa, nullptr, argv.data(), environ) == 0) {
+            int st = 0;
+            while (::waitpid(pid, &st, 0) < 0 && errno == EINTR) {}
+            if (WIFEXITED(st) && WEXITSTATUS(st) == 0 && read_file(out, code) && !code->empty()) rc = 0;
+        } else {
+            *log = "could not start " + cc;
+        }
+        posix_spawn_file_actions_destroy(&fa);
+        if (rc != 0) {
+            std::vector<char> l;
+            if (read_file(logf, &l)) log->append(l.begin(), l.end());
+        }
+    }
+    for (const auto& f : files) std::remove(f.c_str());
+    ::rmdir(d.c_str());
+    return rc;
+}
+
 std::mutex g_jit_mu;   // one compile at a time per process (hipRTC holds a lot of memory)
 std::mutex g_mods_mu;  // the loaded modules (jit_prof_read)
 std::vector<hipModule_t> g_mods;
@@ -203,14 +312,14 @@ std::string jit_source_tag() {
     return buf;
 }
 
-std::string jit_key(const Geo& g, int waves_1level, const std::string& arch) {
+std::string jit_key(const Geo& g, int waves_1level, const std::string& arch, int part, int cc) {
     uint64_t h = fnv1a("primeuncore-jit-2");
     for (int i = 0; i < pu_jit_nsrc; i++) {
         h = fnv1a(pu_jit_src_name[i], h);
         h = fnv1a(pu_jit_src_text[i], h);
     }
     h = fnv1a(geo_cxx(g), h);
-    for (const auto& o : options(arch, waves_1level)) h = fnv1a(o, h);
+    for (const auto& o : options(arch, waves_1level, part, g.num_levels == 1, cc)) h = fnv1a(o, h);
     int maj = 0, min = 0;
     hiprtcVersion(&maj, &min);
     h = fnv1a(std::to_string(maj) + "." + std::to_string(min), h);
@@ -236,16 +345,20 @@ std::string device_arch() {
 }
 
 // Compile configuration g for arch into the cache; 0 or -1 (log filled).
-int compile_into(const Geo& g, int waves, const std::string& arch, const std::string& path,
+int compile_into(const Geo& g, int waves, const std::string& arch, int part, int cc, const std::string& path,
                  std::vector<char>* code, std::string* log) {
-    if (compile(geo_cxx(g), options(arch, waves), code, log) != 0) return -1;
+    const std::vector<std::string> opts = options(arch, waves, part, g.num_levels == 1, cc);
+    const int rc = cc == kJitOffline ? compile_offline(offline_cc(), geo_cxx(g), opts, code, log)
+                                     : compile(geo_cxx(g), opts, code, log);
+    if (rc != 0) return -1;
     ::mkdir(cache_dir().c_str(), 0755);
     write_file_atomic(path, *code);
     return 0;
 }
 
-// Load the kernels from a code object; false (module unloaded) on failure.
-bool load_module(const std::vector<char>& code, JitKernels* out, std::string* why) {
+// Load part `part`'s kernels (f[s][part]) from a code object; false (module
+// unloaded) on failure.
+bool load_module(const std::vector<char>& code, int part, JitKernels* out, std::string* why) {
     hipModule_t mod = nullptr;
     if (hipModuleLoadData(&mod, code.data()) != hipSuccess) {
         *why = "the device refused the code object";
@@ -255,15 +368,57 @@ bool load_module(const std::vector<char>& code, JitKernels* out, std::string* wh
                                       {"pu_jit_uncore_s1_h0", "pu_jit_uncore_s1_h1"},
                                       {"pu_jit_uncore_s2_h0", nullptr}};
     for (int s = 0; s < 3; s++)
-        for (int h = 0; h < 2; h++)
-            if (names[s][h] && hipModuleGetFunction(&out->f[s][h], mod, names[s][h]) != hipSuccess) {
-                (void)hipModuleUnload(mod);
-                *why = std::string("the code object lacks ") + names[s][h];
-                return false;
-            }
-    out->mod = mod;
+        if (names[s][part] && hipModuleGetFunction(&out->f[s][part], mod, names[s][part]) != hipSuccess) {
+            (void)hipModuleUnload(mod);
+            *why = std::string("the code object lacks ") + names[s][part];
+            return false;
+        }
+    out->mod[part] = mod;
     std::lock_guard<std::mutex> lk(g_mods_mu);
     g_mods.push_back(mod);
+    return true;
+}
+
+// Part `part` of configuration g: from the cache, else compiled into it, then
+// loaded; false after a message (the caller falls back to the ahead-of-time
+// kernels).
+bool load_part(const Geo& g, int waves, const std::string& arch, int part, JitKernels* out, bool verbose,
+               std::string* key_out) {
+    std::vector<char> code;
+    std::string log, why;
+    // the offline compiler's code object (written at build time: jit_warm), else hipRTC's
+    for (int cc : {kJitOffline, kJitRtc}) {
+        const std::string key = jit_key(g, waves, arch, part, cc);
+        const std::string path = cache_dir() + "/" + key + ".hsaco";
+        if (!read_file(path, &code)) continue;
+        ::utime(path.c_str(), nullptr);          // in use: tools/jit_warm.py keeps what is used
+        if (load_module(code, part, out, &why)) {
+            *key_out = key;
+            out->cc[part] = cc;
+            return true;
+        }
+        // a damaged or foreign cache entry: drop it (hipRTC compiles it again below)
+        std::fprintf(stderr, "[primeuncore] cached code object %s: %s; compiling it again\n", path.c_str(),
+                     why.c_str());
+        std::remove(path.c_str());
+    }
+    const std::string key = jit_key(g, waves, arch, part, kJitRtc);
+    const std::string path = cache_dir() + "/" + key + ".hsaco";
+    *key_out = key;
+    if (verbose) std::fprintf(stderr, "[primeuncore] compiling the engine for this configuration (%s)\n", key.c_str());
+    if (compile_into(g, waves, arch, part, kJitRtc, path, &code, &log) != 0) {
+        std::fprintf(stderr,
+                     "[primeuncore] compile-time configuration unavailable (hipRTC failed); the ahead-of-time "
+                     "kernels run instead:\n%s\n",
+                     log.c_str());
+        return false;
+    }
+    if (!load_module(code, part, out, &why)) {
+        std::fprintf(stderr, "[primeuncore] freshly compiled code object %s: %s; the ahead-of-time kernels run "
+                             "instead\n", path.c_str(), why.c_str());
+        std::remove(path.c_str());
+        return false;
+    }
     return true;
 }
 }  // namespace
@@ -273,42 +428,16 @@ int jit_load(const Geo& g, JitKernels* out, bool verbose) {
     if (!jit_enabled()) return 0;
     const int waves = jit_waves();
     const std::string arch = device_arch();
-    const std::string key = jit_key(g, waves, arch);
-    const std::string path = cache_dir() + "/" + key + ".hsaco";
+    g_gpu_used = true;
     std::lock_guard<std::mutex> lk(g_jit_mu);   // one compile at a time; another thread may have built it
-    std::vector<char> code;
-    const bool cached = read_file(path, &code);
-    std::string log, why;
-    if (cached) {
-        ::utime(path.c_str(), nullptr);          // in use: tools/jit_warm.py keeps what is used
-        if (load_module(code, out, &why)) {
-            out->ok = true;
-            out->key = key;
+    std::string key[kJitParts];
+    for (int part = 0; part < kJitParts; part++)
+        if (!load_part(g, waves, arch, part, out, verbose, &key[part])) {
+            jit_unload(out);
             return 0;
         }
-        // a damaged or foreign cache entry: drop it and compile once more
-        std::fprintf(stderr, "[primeuncore] cached code object %s: %s; compiling it again\n", path.c_str(),
-                     why.c_str());
-        std::remove(path.c_str());
-        *out = JitKernels{};
-    }
-    if (verbose) std::fprintf(stderr, "[primeuncore] compiling the engine for this configuration (%s)\n", key.c_str());
-    if (compile_into(g, waves, arch, path, &code, &log) != 0) {
-        std::fprintf(stderr,
-                     "[primeuncore] compile-time configuration unavailable (hipRTC failed); the ahead-of-time "
-                     "kernels run instead:\n%s\n",
-                     log.c_str());
-        return 0;
-    }
-    if (!load_module(code, out, &why)) {
-        std::fprintf(stderr, "[primeuncore] freshly compiled code object %s: %s; the ahead-of-time kernels run "
-                             "instead\n", path.c_str(), why.c_str());
-        std::remove(path.c_str());
-        *out = JitKernels{};
-        return 0;
-    }
     out->ok = true;
-    out->key = key;
+    out->key = key[0] + "+" + key[1].substr(key[1].find('-') + 1);
     return 0;
 }
 
@@ -316,26 +445,40 @@ int jit_load(const Geo& g, JitKernels* out, bool verbose) {
 // warm-up), so it targets the architecture the library is built for.
 int jit_warm(const Geo& g, std::string* key_out) {
     const int waves = jit_waves();
-    const std::string key = jit_key(g, waves, kBuildArch);
-    if (key_out) *key_out = key;
-    const std::string path = cache_dir() + "/" + key + ".hsaco";
-    struct stat st;
-    if (::stat(path.c_str(), &st) == 0 && st.st_size > 0) {
-        ::utime(path.c_str(), nullptr);   // still in use (tools/jit_warm.py prunes what is not)
-        return 1;
+    // the offline compiler when present (and this process has put nothing on
+    // the GPU), else hipRTC; a part already cached under either is kept
+    const bool offline = !g_gpu_used && !offline_cc().empty();
+    std::lock_guard<std::mutex> lk(g_jit_mu);
+    int cached = 0;
+    for (int part = 0; part < kJitParts; part++) {
+        const std::string ko = jit_key(g, waves, kBuildArch, part, kJitOffline);
+        const std::string kr = jit_key(g, waves, kBuildArch, part, kJitRtc);
+        const std::string po = cache_dir() + "/" + ko + ".hsaco", pr = cache_dir() + "/" + kr + ".hsaco";
+        struct stat st;
+        const bool have_o = ::stat(po.c_str(), &st) == 0 && st.st_size > 0;
+        const bool have_r = !have_o && ::stat(pr.c_str(), &st) == 0 && st.st_size > 0;
+        if (key_out && part == 0) *key_out = have_o || offline ? ko : kr;
+        if (have_o || (have_r && !offline)) {
+            ::utime((have_o ? po : pr).c_str(), nullptr);   // still in use (tools/jit_warm.py prunes what is not)
+            cached++;
+            continue;
+        }
+        std::vector<char> code;
+        std::string log;
+        const int cc = offline ? kJitOffline : kJitRtc;
+        if (compile_into(g, waves, kBuildArch, part, cc, cc == kJitOffline ? po : pr, &code, &log) != 0)
+            return set_error(PU_EIO, std::string(cc == kJitOffline ? "hipcc: " : "hipRTC: ") + log);
     }
-    std::vector<char> code;
-    std::string log;
-    if (compile_into(g, waves, kBuildArch, path, &code, &log) != 0) return set_error(PU_EIO, "hipRTC: " + log);
-    return 0;
+    return cached == kJitParts ? 1 : 0;
 }
 
 void jit_unload(JitKernels* k) {
-    if (k->mod) {
+    for (hipModule_t& m : k->mod) {
+        if (!m) continue;
         {
             std::lock_guard<std::mutex> lk(g_mods_mu);
             for (size_t i = 0; i < g_mods.size(); i++)
-                if (g_mods[i] == k->mod) {
+                if (g_mods[i] == m) {
                     g_mods.erase(g_mods.begin() + (long)i);
                     break;
                 }
@@ -343,7 +486,7 @@ void jit_unload(JitKernels* k) {
             // the counters are read)
             hipDeviceptr_t p = nullptr;
             size_t bytes = 0;
-            if (hipModuleGetGlobal(&p, &bytes, k->mod, "g_prof") != hipSuccess || !p) {
+            if (hipModuleGetGlobal(&p, &bytes, m, "g_prof") != hipSuccess || !p) {
                 (void)hipGetLastError();
             } else if (hipDeviceSynchronize() == hipSuccess) {
                 std::vector<unsigned long long> buf(bytes / sizeof(unsigned long long), 0);
@@ -353,7 +496,8 @@ void jit_unload(JitKernels* k) {
                 }
             }
         }
-        (void)hipModuleUnload(k->mod);
+        (void)hipModuleUnload(m);
+        m = nullptr;
     }
     *k = JitKernels{};
 }

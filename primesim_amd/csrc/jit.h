@@ -13,8 +13,15 @@ namespace pu {
 // The launch shapes of the engine compiled for one configuration: fixed
 // ranges / time-sliced / replica pool (f[0..2]) x queue headers in HBM or in
 // LDS (f[.][0..1]; the pool runs with headers in HBM only).
+// Code objects come from the offline compiler (hipcc, at build time: jit_warm)
+// or from hipRTC (in-process, on a cache miss at run time).
+constexpr int kJitRtc = 0, kJitOffline = 1;
+// Two code objects per configuration (jit.cpp): part 0 the throughput
+// kernels (f[s][0]), part 1 the latency kernels (f[s][1]).
+constexpr int kJitParts = 2;
 struct JitKernels {
-    hipModule_t mod = nullptr;
+    hipModule_t mod[kJitParts] = {nullptr, nullptr};
+    int cc[kJitParts] = {0, 0};   // kJitRtc / kJitOffline: which compiler built each part
     hipFunction_t f[3][2] = {{nullptr, nullptr}, {nullptr, nullptr}, {nullptr, nullptr}};
     bool ok = false;
     std::string key;
@@ -22,7 +29,7 @@ struct JitKernels {
 
 bool jit_enabled();
 std::string jit_source_tag();
-std::string jit_key(const Geo& g, int waves_1level, const std::string& arch);
+std::string jit_key(const Geo& g, int waves_1level, const std::string& arch, int part, int cc);
 // Load (compiling on a cache miss) the kernels of configuration g; leaves
 // out->ok false, after a message, when the specialisation is off or fails.
 int jit_load(const Geo& g, JitKernels* out, bool verbose);

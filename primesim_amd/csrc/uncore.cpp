@@ -534,6 +534,9 @@ int pu_config_jit_warm(const pu_sim_cfg* cfg) {
 }
 
 int pu_compiled_config(const pu_handle* h) { return h && h->jit.ok ? (h->jit_throughput ? 2 : 1) : 0; }
+int pu_compiled_compiler(const pu_handle* h) {
+    return h && h->jit.ok ? (h->jit.cc[0] == pu::kJitOffline ? 2 : 1) : 0;
+}
 
 const char* pu_jit_source_tag(void) {
     static const std::string tag = pu::jit_source_tag();

@@ -58,6 +58,7 @@ def lib() -> C.CDLL:
         "pu_config_geo_source": (C.c_long, [P(A.SimCfg), C.c_char_p, C.c_size_t]),
         "pu_config_jit_warm": (C.c_int, [P(A.SimCfg)]),
         "pu_compiled_config": (C.c_int, [C.c_void_p]),
+        "pu_compiled_compiler": (C.c_int, [C.c_void_p]),
         "pu_jit_source_tag": (C.c_char_p, []),
         "pu_jit_prof_read": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]),
         "pu_destroy": (None, [C.c_void_p]),

@@ -36,6 +36,7 @@ class StubDevice:
         self.R, self.um, self.dev, self.stream = REPLICAS, StubUM(), None, None
         self.slots = REPLICAS
         self.compiled = 0
+        self.compiler = 0
 
     def headline(self, args, rank, world, keep):
         import oracle as O

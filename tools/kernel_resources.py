@@ -31,9 +31,10 @@ def resources(preset: str, lib: str | None = None) -> dict:
         r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True)
         if r.returncode != 0:
             raise SystemExit(r.stderr[-3000:])
-        (hsaco,) = glob.glob(os.path.join(d, "*.hsaco"))
-        notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", hsaco], capture_output=True,
-                               text=True).stdout
+        # two code objects per configuration (jit.cpp: throughput and latency kernels)
+        notes = "".join(subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", hsaco],
+                                       capture_output=True, text=True).stdout
+                        for hsaco in sorted(glob.glob(os.path.join(d, "*.hsaco"))))
     # one map per kernel, keys in alphabetical order (.agpr_count first, .name
     # in the middle): a kernel's entry starts at its .agpr_count line
     out: dict = {}

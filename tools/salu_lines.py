@@ -76,9 +76,9 @@ def compile_lines(preset: str) -> str:
         r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True)
         if r.returncode != 0:
             raise SystemExit(r.stderr[-3000:])
-        (hsaco,) = glob.glob(os.path.join(d, "*.hsaco"))
-        return subprocess.run([OBJDUMP, "-d", "-l", "--no-show-raw-insn", hsaco], capture_output=True,
-                              text=True).stdout
+        # two code objects per configuration (jit.cpp: throughput and latency kernels)
+        return "".join(subprocess.run([OBJDUMP, "-d", "-l", "--no-show-raw-insn", hsaco], capture_output=True,
+                                      text=True).stdout for hsaco in sorted(glob.glob(os.path.join(d, "*.hsaco"))))
 
 
 def tally(dis: str, kernel: str):

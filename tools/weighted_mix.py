@@ -40,15 +40,16 @@ from salu_lines import klass  # noqa: E402
 ENGINE = os.path.join(ROOT, "primesim_amd", "csrc", "engine.hip")
 
 
-def build_hsaco(preset: str, d: str) -> str:
-    env = dict(os.environ, PRIMEUNCORE_JIT_CACHE=d, PRIMEUNCORE_JIT_EXTRA="-gline-tables-only")
+def build_hsaco(preset: str, d: str, extra: str = "", kernel: str = "pu_jit_uncore_s2_h0") -> str:
+    env = dict(os.environ, PRIMEUNCORE_JIT_CACHE=d, PRIMEUNCORE_JIT_EXTRA=("-gline-tables-only " + extra).strip())
     code = ("import ctypes as C, sys; sys.path.insert(0, %r); import primesim_amd as P; "
             "from primesim_amd import config as CF, uncore; cfg = P.config_from_dict(CF.preset(%r)); "
             "rc = uncore.lib().pu_config_jit_warm(C.byref(cfg)); sys.exit(0 if rc >= 0 else 1)") % (ROOT, preset)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True)
     if r.returncode != 0:
         raise SystemExit(r.stderr[-3000:])
-    (hsaco,) = glob.glob(os.path.join(d, "*.hsaco"))
+    # two code objects per configuration (jit.cpp): the one holding the kernel
+    (hsaco,) = [f for f in glob.glob(os.path.join(d, "*.hsaco")) if kernel.encode() in open(f, "rb").read()]
     return hsaco
 
 
@@ -186,10 +187,11 @@ def main() -> None:
     ap.add_argument("--sq", default=os.path.join(ROOT, "profiles", "r4n_sq.json"),
                     help="SQ counters of the same kernel: measured VALU/SALU per access to compare with")
     ap.add_argument("--json", default="")
+    ap.add_argument("--extra", default="", help="more compile options for the compiled configuration")
     a = ap.parse_args()
 
     with tempfile.TemporaryDirectory(prefix="pu_wmix_") as d:
-        hsaco = build_hsaco(a.preset, d)
+        hsaco = build_hsaco(a.preset, d, a.extra, a.kernel)
         ins = instructions(hsaco, a.kernel)
         ch = chains(hsaco, [x for x, _ in ins])
     assert len(ch) == len(ins), (len(ch), len(ins))
