@@ -84,6 +84,11 @@ STAGE_GROUP = 256       # replicas whose requests the host generates per staging
 BUSY_MIN = 0.95         # a replica pool busier than this kept every slot resident for the whole slice
 
 
+def timed_req_bytes(args) -> int:
+    """Bytes per request record of the timed window (pu_req16 or pu_req)."""
+    return 16 if getattr(args, "req_format", 32) == 16 else REQ_BYTES
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -352,13 +357,15 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
     offs = torch.from_numpy((np.arange(R + 1, dtype=np.uint64) * np.uint64(args.chunk)).view(np.int64)).to(dev)
     kept = {r: [] for r in keep}
 
-    def next_chunk() -> torch.Tensor:
-        out = torch.empty((R, args.chunk * REQ_BYTES), dtype=torch.uint8, device=dev)
+    def next_chunk(rb: int = REQ_BYTES) -> torch.Tensor:
+        # rb = 16: the chunk as pu_req16 records (pack_req16 refuses what does not fit)
+        out = torch.empty((R, args.chunk * rb), dtype=torch.uint8, device=dev)
         for k, gen in enumerate(gens):
             n = len(gen)
             got = gen.next_into(host[:n])
             assert got == args.chunk, (got, args.chunk)
-            out[k * G:k * G + n].copy_(torch.from_numpy(host[:n].view(np.uint8).reshape(n, -1)))
+            rec = host[:n] if rb == REQ_BYTES else P.uncore.pack_req16(host[:n])
+            out[k * G:k * G + n].copy_(torch.from_numpy(rec.view(np.uint8).reshape(n, -1)))
         return out.view(-1)
 
     d_warm_delay = torch.zeros(R * args.chunk, dtype=torch.int32, device=dev)
@@ -376,9 +383,13 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
         (L.pu_jit_prof_read if os.environ.get("PU_PROF_JIT") else L.pu_engine_prof_read)(None, 0, 1)
     t_gen = time.time()
     W_t = steps * args.chunk
-    d_win = torch.empty((R, W_t, REQ_BYTES), dtype=torch.uint8, device=dev)
+    # the timed window as 16-B records (--req-format 16): 20 B a request with
+    # its delay instead of 36, so the driver's 20-step window fits a replica
+    # pool over every resident wavefront in HBM
+    rb = timed_req_bytes(args)
+    d_win = torch.empty((R, W_t, rb), dtype=torch.uint8, device=dev)
     for k in range(steps):
-        d_win[:, k * args.chunk:(k + 1) * args.chunk, :] = next_chunk().view(R, args.chunk, REQ_BYTES)
+        d_win[:, k * args.chunk:(k + 1) * args.chunk, :] = next_chunk(rb).view(R, args.chunk, rb)
     for gen in gens:
         gen.close()
     d_win_delay = torch.zeros(R * W_t, dtype=torch.int32, device=dev)
@@ -397,6 +408,7 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
 
     # HIP events on the engine's (non-null) stream time exactly its launches
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    um.set_device_req_format(P.uncore.PU_REQ_FMT_16 if rb == 16 else P.uncore.PU_REQ_FMT_32)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -417,6 +429,7 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    um.set_device_req_format(P.uncore.PU_REQ_FMT_32)
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     log(f"[bench] timed {steps} steps in {elapsed:.3f}s; per-launch ms {['%.1f' % x for x in kern_ms]}")
     pos = d_pos.cpu().numpy().view(np.uint64)
@@ -549,6 +562,10 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=10, help="timed steps")
     ap.add_argument("--warmup", type=int, default=10, help="untimed steps of --chunk requests per replica")
     ap.add_argument("--replicas", type=int, default=0, help="replicas per GPU (0 = size to HBM)")
+    ap.add_argument("--req-format", type=int, choices=(16, 32), default=16,
+                    help="timed-window request records: 16-B pu_req16 (pu_pack_req16) or 32-B pu_req")
+    ap.add_argument("--slots", type=int, default=int(os.environ.get("PU_BENCH_SLOTS", "0")),
+                    help="wavefront slots per GPU (0 = every replica slot the kernel keeps resident)")
     ap.add_argument("--spare-replicas", type=float, default=0.1,
                     help="replicas beyond the resident wavefront slots, as a fraction of them (replica pool)")
     ap.add_argument("--chunk", type=int, default=40960, help="requests per replica per step")
@@ -587,13 +604,15 @@ class Device:
         probe.close()
         # ranks rehearsed on one card (PU_BENCH_DEVICE) split its memory and waves
         share = int(os.environ.get("LOCAL_WORLD_SIZE", "1")) if "PU_BENCH_DEVICE" in os.environ else 1
-        per_bytes = rbytes + (args.steps + 1) * args.chunk * (REQ_BYTES + 4)
+        per_bytes = rbytes + args.steps * args.chunk * (timed_req_bytes(args) + 4) + args.chunk * (REQ_BYTES + 4)
         free, _ = torch.cuda.mem_get_info(self.dev)
         # one wavefront per replica slot the kernel keeps resident, and up to
         # --spare-replicas more replicas (as HBM allows) for the replica pool:
         # a wavefront whose replica halts or finishes its window takes an
         # unstarted one (pu_run_device_pool), so no slot idles
         res = max(1, resident // share)
+        if args.slots:
+            res = min(res, args.slots)
         fit = int((free * 0.88 / share) // per_bytes)
         R = args.replicas or max(1, min(int(res * (1.0 + args.spare_replicas)), fit))
         R = max(1, R - R % 8) if R >= 8 else R
@@ -816,6 +835,7 @@ def main(argv=None) -> None:
                          f"fixed: {args.chunk} requests per replica per launch"),
                 "mean_requests_per_replica_per_step": H.processed / (R * args.steps),
                 "warmup_requests_per_replica": args.warmup * args.chunk,
+                "timed_request_record_bytes": timed_req_bytes(args),
                 "parallelism": (f"replicas: {R} independent uncores per GPU ({D.slots} simulated at once, one "
                                 f"wavefront each) x {world} GPU(s), one process per GPU, no data-path collective "
                                 f"({args.dist_backend} for the barrier and the max/sum reduction only)" if world > 1 else

@@ -154,6 +154,27 @@ typedef struct pu_req {
     int32_t  _pad1;
 } pu_req;                  /* 32 bytes */
 
+/* Compact 16-byte device request record for throughput runs whose requests
+ * fit (no reference counterpart: a layout of the same MsgMem fields).
+ *   a = addr_dmem
+ *   b = timer (bits 0-39) | core (40-55) | prog_id (56-61) | mem_type (62)
+ *       | batch_start (63);  tag is 0.
+ * pu_pack_req16 packs n records and returns 0, or PU_ERANGE (out untouched
+ * past the record it names in the error text) at the first that does not
+ * fit: timer outside [0, 2^40), core outside [0, 2^16), prog_id outside
+ * [0, 64), mem_type or batch_start above 1, or tag != 0.
+ * pu_set_device_req_format(h, PU_REQ_FMT_16) makes pu_run_device,
+ * pu_run_device_sliced and pu_run_device_pool read d_reqs as pu_req16
+ * records (indices in d_off / d_pos count records either way); those runs
+ * use the throughput kernels (a latency launch's helper reads pu_req).
+ * Results are identical to the same requests as pu_req.  PU_REQ_FMT_32
+ * (the default) restores pu_req.  The host batch paths always take pu_req. */
+typedef struct pu_req16 {
+    uint64_t a, b;
+} pu_req16;
+#define PU_REQ_FMT_32 0
+#define PU_REQ_FMT_16 1
+
 /* ------------------------------------------------------------------------
  * Statistics — every number System::report prints (reference
  * src/system.cpp:956-1111, network.cpp:310-323, dram.cpp:50-55) plus the
@@ -377,6 +398,8 @@ int  pu_pool_slots(pu_handle* h);
 long pu_pool_words(int slots);
 int  pu_run_device_pool(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
                         uint64_t* d_pos, uint32_t* d_sched, int slots, uint64_t budget_us, void* hip_stream);
+int pu_set_device_req_format(pu_handle* h, int fmt);
+int pu_pack_req16(const pu_req* in, size_t n, pu_req16* out);
 int pu_synchronize(pu_handle* h);
 
 /* Per-core completion cycle of the last request each core issued

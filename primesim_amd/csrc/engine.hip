@@ -2512,6 +2512,22 @@ __device__ __forceinline__ void hdr_image_out(char* qhdr, uint32_t nqueues, uint
     for (uint32_t k = t; k < nqueues * PU_LDS_SLOT; k += 128) gh[k] = lds_qhdr[k];
 }
 
+// A 16-B request record (pu_req16, primeuncore.h): a = addr_dmem; b = timer
+// (bits 0-39) | core (40-55) | prog_id (56-61) | mem_type (62) | batch_start
+// (63); tag 0.  pu_pack_req16 refuses what does not fit, so this is exact.
+__device__ __forceinline__ pu_req req_unpack16(v2u64 w) {
+    pu_req q;
+    q.addr = w.x;
+    q.timer = (int64_t)(w.y & ((1ull << 40) - 1));
+    q.core = (int32_t)((w.y >> 40) & 0xFFFFu);
+    q.prog_id = (int32_t)((w.y >> 56) & 63u);
+    q.mem_type = (uint8_t)((w.y >> 62) & 1u);
+    q.batch_start = (uint8_t)(w.y >> 63);
+    q.tag = 0;
+    q._pad1 = 0;
+    return q;
+}
+
 // One replica's message loop (prime.cpp:120-137): reqs[b .. end) in order, D
 // restarting at each batch_start; d = access(core, req, timer + D); D += d - 1.
 // e.base is the replica's arena.  Time-sliced launches (deadline != MAX) stop
@@ -2554,9 +2570,9 @@ __device__ __forceinline__ bool replica_loop(Engine<NL, LH>& e, const pu_req* __
         if (SLICED && __builtin_amdgcn_s_memrealtime() >= uni64(lds_ctl.deadline)) break;
         if (uni32((uint32_t)lds_ctl.halted)) break;   // the rest is zero-filled below
         PROF_T(p_loop);
-        const pu_req q = reqs[i];
-        const bool core_ok = q.core >= 0 && q.core < e.g->num_cores;
         const uint32_t fl = uni32(lds_ctl.flags);
+        const pu_req q = (fl & PU_KF_REQ16) ? req_unpack16(reinterpret_cast<const v2u64*>(reqs)[i]) : reqs[i];
+        const bool core_ok = q.core >= 0 && q.core < e.g->num_cores;
         if (e.ln == 0) lds_ctl.cur = i;
         if (q.batch_start && e.ln == 0) {
             lds_ctl.D = 0;

@@ -204,6 +204,8 @@ struct Geo {
                             // with num_recv_threads > 1)
 #define PU_KF_CLOSED   4u   // closed-loop replay: timer_i += the core's earlier batch delays
                             // (core_manager.cpp:265 `cycle += delay` after each reply)
+#define PU_KF_REQ16    8u   // d_reqs holds 16-B pu_req16 records (pu_set_device_req_format;
+                            // throughput launches only)
 
 // Per-replica run state carried across launches.
 struct RunState {

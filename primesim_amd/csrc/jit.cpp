@@ -10,8 +10,8 @@
 // has put nothing on the GPU) the ROCm driver hipcc in a child process; on a
 // cache miss at run time hipRTC in-process.  The same source and options give
 // different code: at C4 hipcc's throughput kernel needs 76 VGPRs and spills
-// none where hipRTC's needs 80 and spills 11, +4.6% on the headline, same box
-// (profiles/r5l_ab_ens.txt); so the cache prefers hipcc's object.  Constant
+// none where hipRTC's needs 80 and spills 11, +4.7% on the headline, same box
+// (profiles/r5m_ab_ens.txt); so the cache prefers hipcc's object.  Constant
 // geometry removes the kernel's scalar loads of its configuration and the
 // scalar address arithmetic around them, the largest part of the lone wave's
 // issue and wait time.

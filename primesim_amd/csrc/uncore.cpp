@@ -290,6 +290,7 @@ struct pu_handle {
     double last_ms = 0.0;
     struct timespec sim_start{}, sim_finish{};   // UncoreManager::sim_start_time / sim_finish_time
     uint32_t replay_flags = 0;   // PU_KF_CLOSED under PU_REPLAY_CLOSED
+    uint32_t dev_req_flags = 0;  // PU_KF_REQ16 under PU_REQ_FMT_16 (the device-run entry points)
     int cus = 0;                 // compute units of the device (latency-mode launches)
     bool lds_headers_ok = false; // the replica's queue headers fit one CU's LDS
     bool lds_headers_short = false;   // latency mode for short host batches too
@@ -408,7 +409,9 @@ int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const 
     // (a lone uncore_access, one MEM_REQUESTS message) wins back, so those
     // run with the headers in HBM (tools/latency_bench.py)
     // (a replica-pool launch is always a throughput launch)
-    const int lh = h->lds_headers_ok && nblocks <= h->cus && !short_launch && !d_sched ? 1 : 0;
+    // (16-B request records: throughput kernels only, the latency helper reads pu_req)
+    const int lh = h->lds_headers_ok && nblocks <= h->cus && !short_launch && !d_sched &&
+                   !(extra_flags & PU_KF_REQ16) ? 1 : 0;
     const uint32_t flags = (extra_flags & PU_KF_NOHALT) || !use_replay_mode ? extra_flags
                                                                           : (h->replay_flags | extra_flags);
     // latency launches run the compiled configuration (one simulation alone +23%
@@ -851,7 +854,28 @@ int pu_run_device(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off, int
     if (!h || !d_reqs || !d_off || !d_delay) return pu::set_error(PU_EINVAL, "bad arguments");
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
     std::lock_guard<std::mutex> lk(h->mu);
-    return launch(h, 0, h->R, d_reqs, d_off, d_delay, s);
+    return launch(h, 0, h->R, d_reqs, d_off, d_delay, s, nullptr, 0, h->dev_req_flags);
+}
+
+int pu_set_device_req_format(pu_handle* h, int fmt) {
+    if (!h || (fmt != PU_REQ_FMT_32 && fmt != PU_REQ_FMT_16)) return pu::set_error(PU_EINVAL, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->dev_req_flags = fmt == PU_REQ_FMT_16 ? PU_KF_REQ16 : 0u;
+    return 0;
+}
+
+int pu_pack_req16(const pu_req* in, size_t n, pu_req16* out) {
+    if (n && (!in || !out)) return pu::set_error(PU_EINVAL, "bad arguments");
+    for (size_t i = 0; i < n; i++) {
+        const pu_req& q = in[i];
+        if (q.timer < 0 || q.timer >= (int64_t)1 << 40 || q.core < 0 || q.core >= 1 << 16 || q.prog_id < 0 ||
+            q.prog_id >= 64 || q.mem_type > 1 || q.batch_start > 1 || q.tag != 0)
+            return pu::set_error(PU_ERANGE, "request " + std::to_string(i) + " does not fit pu_req16");
+        out[i].a = q.addr;
+        out[i].b = (uint64_t)q.timer | (uint64_t)(uint32_t)q.core << 40 | (uint64_t)(uint32_t)q.prog_id << 56 |
+                   (uint64_t)q.mem_type << 62 | (uint64_t)q.batch_start << 63;
+    }
+    return 0;
 }
 
 }  // extern "C"
@@ -881,7 +905,8 @@ int pu_run_device_sliced(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_o
     if (!h || !d_reqs || !d_off || !d_delay || !d_pos) return pu::set_error(PU_EINVAL, "bad arguments");
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
     std::lock_guard<std::mutex> lk(h->mu);
-    return launch(h, 0, h->R, d_reqs, d_off, d_delay, s, d_pos, budget_us * 100);   // s_memrealtime: 100 MHz
+    return launch(h, 0, h->R, d_reqs, d_off, d_delay, s, d_pos, budget_us * 100,   // s_memrealtime: 100 MHz
+                  h->dev_req_flags);
 }
 
 int pu_pool_slots(pu_handle* h) {
@@ -903,7 +928,8 @@ int pu_run_device_pool(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off
         return pu::set_error(PU_ERANGE, "slots must be 1.." + std::to_string(most) + " (pu_pool_slots)");
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
     std::lock_guard<std::mutex> lk(h->mu);
-    return launch(h, 0, slots, d_reqs, d_off, d_delay, s, d_pos, budget_us * 100, 0, false, true, d_sched);
+    return launch(h, 0, slots, d_reqs, d_off, d_delay, s, d_pos, budget_us * 100, h->dev_req_flags, false, true,
+                  d_sched);
 }
 
 int pu_synchronize(pu_handle* h) {

@@ -83,6 +83,8 @@ def lib() -> C.CDLL:
         "pu_run_device_pool": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_int, C.c_uint64, C.c_void_p]),
         "pu_synchronize": (C.c_int, [C.c_void_p]),
+        "pu_set_device_req_format": (C.c_int, [C.c_void_p, C.c_int]),
+        "pu_pack_req16": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p]),
         "pu_core_completion": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
         "pu_stats_get": (C.c_int, [C.c_void_p, C.c_int, P(A.Stats)]),
         "pu_report": (C.c_long, [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_size_t]),
@@ -150,6 +152,7 @@ def last_error() -> str:
 # wrapped delay may collide with one); the mirror uses pu_access_status.
 PU_ERRORS = (-5, -12, -19, -22, -34, -71, -95)
 PU_REPLAY_OPEN, PU_REPLAY_CLOSED = 0, 1
+PU_REQ_FMT_32, PU_REQ_FMT_16 = 0, 1
 
 
 def library_source_hash() -> str:
@@ -198,6 +201,16 @@ class StreamSpec:
     def params(self) -> A.StreamParams:
         return A.StreamParams(self.kind, self.num_cores, self.seed, self.quantum, self.num_quanta,
                               self.max_msg, self.num_progs, self.max_requests, self.write_pct, 0)
+
+
+def pack_req16(reqs: np.ndarray) -> np.ndarray:
+    """REQ_DTYPE records -> 16-B pu_req16 records (uint64 pairs, primeuncore.h);
+    raises UncoreError naming the first record that does not fit."""
+    assert reqs.dtype == A.REQ_DTYPE and reqs.flags.c_contiguous
+    out = np.empty(reqs.shape + (2,), dtype=np.uint64)
+    if lib().pu_pack_req16(reqs.ctypes.data, reqs.size, out.ctypes.data) != 0:
+        raise UncoreError(last_error())
+    return out
 
 
 def generate_stream(spec: StreamSpec) -> np.ndarray:
@@ -444,6 +457,12 @@ class UncoreManager:
         """PU_REPLAY_OPEN (recorded timers) or PU_REPLAY_CLOSED (timer_i += the
         core's earlier batch delays, core_manager.cpp:265)."""
         if lib().pu_set_replay_mode(self._handle(), mode) != 0:
+            raise UncoreError(last_error())
+
+    def set_device_req_format(self, fmt: int) -> None:
+        """PU_REQ_FMT_32 (pu_req) or PU_REQ_FMT_16 (pu_req16, pack_req16): the
+        record format run_device / run_device_sliced / run_device_pool read."""
+        if lib().pu_set_device_req_format(self._handle(), fmt) != 0:
             raise UncoreError(last_error())
 
     def error_flags(self, n: Optional[int] = None) -> np.ndarray:
