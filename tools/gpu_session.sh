@@ -20,7 +20,9 @@
 #                (-DPU_PROF through PRIMEUNCORE_JIT_EXTRA), open and closed loop
 #   regions_ens  the same for the throughput kernel at the headline's replica count
 #   ab_modes:V1,V2,...   interleaved same-box A/B of engine libraries (main = libprimeuncore.so, else
-#                libprimeuncore_V.so; V@FLAGS also sets PRIMEUNCORE_JIT_EXTRA=FLAGS, '+' for a space,
+#                libprimeuncore_V.so; V@FLAGS also sets PRIMEUNCORE_JIT_EXTRA=FLAGS, '+' for a space
+#                (compiled by hipRTC on the box unless warmed in-tree first:
+#                PRIMEUNCORE_JIT_EXTRA=FLAGS python3 tools/jit_warm.py --only "preset C4"),
 #                and V#W sets PRIMEUNCORE_JIT_WAVES=W) in three regimes: headline, one simulation
 #                alone open / closed loop
 #   ab_single:V1,V2,...  the same, one simulation alone only

@@ -1,9 +1,12 @@
 """Warm the compile-time-configuration cache (primesim_amd/jit_cache/) for every
 configuration the GPU tests, smoke() and bench.py use: the golden XMLs, the
-C1-C5 presets, the DRAM-bank test geometries and tests/extra_configs.py.  Runs on the CPU (hipRTC needs
-no GPU), several compiles at once; a configuration already cached is skipped.
+C1-C5 presets, the DRAM-bank test geometries and tests/extra_configs.py.  Runs on the CPU (hipcc, in a
+child process of each worker; no GPU), several compiles at once; a configuration already cached is skipped.
+A same-box A/B of compile options (tools/gpu_session.sh V@FLAGS) compiles its variant with hipRTC on the
+GPU box unless the variant is warmed here first with the same environment:
 
-    python3 tools/jit_warm.py [-j N]
+    python3 tools/jit_warm.py [-j N] [--only "preset C4"]
+    PRIMEUNCORE_JIT_EXTRA="..." python3 tools/jit_warm.py --only "preset C4"
 """
 from __future__ import annotations
 
@@ -71,8 +74,9 @@ def _warm(item):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument("--only", default="", help="warm only the configurations whose name contains this")
     a = ap.parse_args()
-    items = [(n, bytes(c)) for n, c in configs()]
+    items = [(n, bytes(c)) for n, c in configs() if a.only in n]
     bad = 0
     t0 = time.time()
     with ProcessPoolExecutor(a.j) as ex:
@@ -90,7 +94,7 @@ def main() -> int:
     intree = os.path.join(ROOT, "primesim_amd", "jit_cache")
     cache = os.environ.get("PRIMEUNCORE_JIT_CACHE") or intree
     stale = []
-    if not bad and os.path.realpath(cache) == os.path.realpath(intree):
+    if not bad and not a.only and os.path.realpath(cache) == os.path.realpath(intree):
         live = live_source_tags()
         # the product library's own tag, read in this process: if it is missing
         # from what the children reported (a child load failed, a library
