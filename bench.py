@@ -564,6 +564,8 @@ def parse_args(argv=None):
     ap.add_argument("--replicas", type=int, default=0, help="replicas per GPU (0 = size to HBM)")
     ap.add_argument("--req-format", type=int, choices=(16, 32), default=16,
                     help="timed-window request records: 16-B pu_req16 (pu_pack_req16) or 32-B pu_req")
+    ap.add_argument("--hbm-fraction", type=float, default=float(os.environ.get("PU_BENCH_HBM_FRACTION", "0.88")),
+                    help="share of the free HBM the replicas and their request windows may take")
     ap.add_argument("--slots", type=int, default=int(os.environ.get("PU_BENCH_SLOTS", "0")),
                     help="wavefront slots per GPU (0 = every replica slot the kernel keeps resident)")
     ap.add_argument("--spare-replicas", type=float, default=0.1,
@@ -613,7 +615,7 @@ class Device:
         res = max(1, resident // share)
         if args.slots:
             res = min(res, args.slots)
-        fit = int((free * 0.88 / share) // per_bytes)
+        fit = int((free * args.hbm_fraction / share) // per_bytes)
         R = args.replicas or max(1, min(int(res * (1.0 + args.spare_replicas)), fit))
         R = max(1, R - R % 8) if R >= 8 else R
         self.slots = min(R, res)

@@ -27,6 +27,7 @@
 #                alone open / closed loop
 #   ab_single:V1,V2,...  the same, one simulation alone only
 #   ab_ens:V1,V2,...     the same, headline only (3 rounds)
+#   ab_driver:V1,V2,...  the headline on the driver's window (--steps 20 --warmup 5), 2 interleaved rounds
 #   refwrap      tools/ref_overhead.py: the reference CPU uncore with and without the golden counting wraps
 #   residency    tools/probe/residency: one-wave workgroups resident per CU by resource shape
 #   diag:V       one headline run (5+5 steps) of variant V (ab syntax) with its bench log kept
@@ -94,6 +95,10 @@ for S in "$@"; do
     ab_modes:*) ab 2 "ens single closed" "${S#ab_modes:}" > ${O}_ab_modes.txt || exit 1;;
     ab_single:*) ab 2 "single closed" "${S#ab_single:}" > ${O}_ab_single.txt || exit 1;;
     ab_ens:*) ab 3 "ens" "${S#ab_ens:}" > ${O}_ab_ens.txt || exit 1;;
+    ab_driver:*) for i in 1 2; do for v in $(echo "${S#ab_driver:}" | tr ',' ' '); do
+               ( variant_env "$v"
+                 timeout -k 10 400 $BENCH $DRIVER --no-cpu --no-extras 2>>${O}_ab.err | python -c "import json,sys; b=json.loads(sys.stdin.read().strip().splitlines()[-1]); c=b['config']; p=c.get('replica_pool') or {}; print('driver', '$v', round(b['value']/1e6,2), 'M/s', 'replicas', c['replicas_per_gpu'], 'slots', c['wavefronts_per_gpu'], 'halted', c['halted_replicas'], 'busy', round(p.get('busy_fraction', 0), 4), 'started', p.get('replicas_started'), flush=True)" >> ${O}_ab_driver.txt ) || exit 1
+             done; done;;
     ab_pool) for i in 1 2 3; do for sp in 0.1 0; do
                timeout -k 10 300 $BENCH $DRIVER --no-cpu --no-extras --spare-replicas $sp 2>>${O}_ab.err | python -c "import json,sys; b=json.loads(sys.stdin.read().strip().splitlines()[-1]); c=b['config']; p=c.get('replica_pool') or {}; print('spare $sp', round(b['value']/1e6,2), 'M/s', 'replicas', c['replicas_per_gpu'], 'halted', c['halted_replicas'], 'busy', round(p.get('busy_fraction', 0), 4), flush=True)" >> ${O}_ab_pool.txt || exit 1
              done; done;;
