@@ -59,3 +59,27 @@ def test_wide_sets_need_the_compiled_configuration(name, monkeypatch):
     um = P.UncoreManager()
     with pytest.raises(Exception, match="more than 64 ways"):
         um.init(P.load_config(Case(name).xml_path), replicas=1)
+
+
+def test_handle_reports_its_compiler(tmp_path, monkeypatch):
+    """The in-tree cache holds hipcc's code objects (build-time warm-up): a
+    handle over it reports compiler 2.  A cache miss at run time (an empty
+    cache directory) is compiled by hipRTC in-process, never by starting a
+    compiler from a process that has used the GPU: compiler 1, and the same
+    delays as the reference."""
+    cfg = P.load_config(Case("c1_hot").xml_path)
+    um = P.UncoreManager()
+    um.init(cfg, replicas=1)
+    try:
+        assert uncore.lib().pu_compiled_compiler(um._handle()) == 2
+    finally:
+        um.close()
+    monkeypatch.setenv("PRIMEUNCORE_JIT_CACHE", str(tmp_path))
+    um = P.UncoreManager()
+    um.init(cfg, replicas=1)
+    try:
+        assert uncore.lib().pu_compiled_compiler(um._handle()) == 1
+    finally:
+        um.close()
+    assert len(list(tmp_path.glob("*.hsaco"))) == 2        # both parts, hipRTC's keys
+    test_engine_reproduces_reference("c1_hot")              # on hipRTC's code objects (the env still points there)
