@@ -165,13 +165,15 @@ struct QState {
 #define PU_RING_PF 3   // staged rings in flight per wave (6 KB LDS: 5 waves/SIMD fit the CU's 160 KB)
 #endif
 // The throughput kernels' own count.  The compiled one-level configuration
-// runs 6 waves per SIMD with 2 staged rings: 5,424 B of LDS per wave = five
-// 1,280-B units, 25 per CU, so all 24 waves reside (3 rings would be six
-// units, 21 per CU); +4.0% on the C4 headline against 5 waves with 3 rings,
-// same box (profiles/r5j_ab_ens.txt).
+// runs 7 waves per SIMD with 1 staged ring: 3,376 B of LDS per wave = three
+// 1,280-B units, so all 28 waves of a CU reside.  6 waves with 2 rings (five
+// units, 25 per CU) was +4.0% on the C4 headline against 5 waves with 3 rings
+// (profiles/r5j_ab_ens.txt); at 6 waves 1 ring equals 2 (r5s_ab_ens_waves7.txt);
+// 7 waves, once the sharer bit below stopped spilling, +4.3% on the driver's
+// 20-step window over 6 (r5w_ab_driver.txt), same box.
 #ifndef PU_RING_PF_TP
 #if defined(PU_JIT_GEO) && PU_JIT_NL == 1
-#define PU_RING_PF_TP 2
+#define PU_RING_PF_TP 1
 #else
 #define PU_RING_PF_TP PU_RING_PF
 #endif
@@ -185,7 +187,7 @@ constexpr int ring_pf() { return LH ? PU_RING_PF : PU_RING_PF_TP; }
 // would spill ~120 VGPRs at 128, so they keep the compiler's choice.
 #ifndef PU_WAVES_1LEVEL
 #if defined(PU_JIT_GEO)
-#define PU_WAVES_1LEVEL 6   // compiled configuration: 76 VGPRs, no spill (jit.cpp's options)
+#define PU_WAVES_1LEVEL 7   // compiled configuration: 72 VGPRs, one 4-B spill (jit.cpp's options)
 #else
 #define PU_WAVES_1LEVEL 5
 #endif
@@ -1752,13 +1754,19 @@ struct Engine {
         }
         uint64_t idx;
         if (!pool_alloc(&idx)) return;
+        // cid through an opaque move: its lane bit is built here, not hoisted
+        // to where cid is first known and held in VGPRs across the probes (at
+        // 7 waves per SIMD two 8-B scratch spills per access: fabric traffic
+        // 1.30x, and 7 waves only +1.2%; profiles/r5u_traffic.json, r5t_ab_driver.txt)
+        int c;
+        asm volatile("s_mov_b32 %0, %1" : "=s"(c) : "s"(cid));
         for (int base = 0; base < g->dir.nwords; base += 64) {
             uint64_t w = 0;
             for (uint32_t i = 0; i < nsh; i++) {
                 int id = (int)((sh >> (16 * i)) & 0xFFFF);
                 if ((id >> 6) == base + ln) w |= 1ull << (id & 63);
             }
-            if ((cid >> 6) == base + ln) w |= 1ull << (cid & 63);
+            if ((c >> 6) == base + ln) w |= 1ull << (c & 63);
             if (base + ln < g->dir.nwords) pool_of(idx)[base + ln] = w;
         }
         nsh = PU_SH_POOL;

@@ -121,10 +121,11 @@ void write_file_atomic(const std::string& path, const std::vector<char>& data) {
 // without machine LICM: hoisted loop invariants (constants, address pairs)
 // were held in SGPRs across the whole request loop and spilled (192 spill
 // slots); rematerialised at their uses the kernel needs 76 VGPRs instead of 96
-// and fits 6 waves per SIMD with no spill.  6 waves + 2 staged rings + this:
-// +4.0% on the C4 headline (profiles/r5j_ab_ens.txt, r5k_ab_ens.txt); the
-// same flag at 5 waves lost 1.2%, and the latency kernels lost 1.5% open /
-// 2% closed loop with it (r5i_ab_nolicm.txt), so part 1 keeps the default.
+// and fits 6 waves per SIMD with no spill (72 and 7 waves since; engine.hip
+// PU_WAVES_1LEVEL).  6 waves + 2 staged rings + this: +4.0% on the C4
+// headline (profiles/r5j_ab_ens.txt, r5k_ab_ens.txt); the same flag at 5
+// waves lost 1.2%, and the latency kernels lost 1.5% open / 2% closed loop
+// with it (r5i_ab_nolicm.txt), so part 1 keeps the default.
 std::vector<std::string> options(const std::string& arch, int waves_1level, int part, bool one_level, int cc) {
     // max-occupancy: at C4 the throughput kernel spills 2 VGPRs instead of 4
     // and ran ahead of max-ILP in each of three interleaved rounds (233.0 /
