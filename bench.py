@@ -69,8 +69,8 @@ LAUNCH_CMD = None       # rank command for launch_ranks (None: this file; tests 
 LAST_REPLICAS = 0       # replicas of the last main() run (tools/prof_regions.py)
 LAST_PER_REPLICA = None  # per-replica stat deltas of the timed steps (profiling runs only)
 METRIC = "simulated memory accesses/sec (uncore) at 1024 cores; % HBM roofline"
-LIMITER = ("dependent-load latency and instruction issue (profiles/r5q_sq.json: 28% of wave cycles issuing, "
-           "40% waiting on memory, 32% in issue stalls at 6 waves/SIMD; fabric traffic under 40% of 8 TB/s), "
+LIMITER = ("dependent-load latency and instruction issue (profiles/r5x_sq.json: 26% of wave cycles issuing, "
+           "38% waiting on memory, 36% in issue stalls at 7 waves/SIMD; fabric traffic about 41% of 8 TB/s), "
            "not HBM bandwidth")
 REQ_BYTES = 32          # sizeof(pu_req)
 VARIANTS = {0: "ahead-of-time kernels (runtime geometry) for every launch",
