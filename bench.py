@@ -44,7 +44,12 @@ At N=1 (rank 0) the same line also carries:
   * roofline.traffic — fabric bytes (FETCH_SIZE + WRITE_SIZE, separate PMC
     passes; includes Infinity-Cache hits) measured by tools/pmc_traffic.py for
     THIS library build only (refused when its source hash differs).
-The run exits non-zero when a parity check fails.
+At N>1 every rank forks --rank-parity-workers reference processes before it
+touches its GPU; they replay that rank's replica 0 and its first replica-pool
+spare, each rank checks their delays against its own, and rank 0's line
+carries `rank_parity` (per rank and overall) and `roofline.job` (algorithmic
+bytes summed over ranks / the slowest rank's mean launch / (N x 8 TB/s)).
+The run exits non-zero when a parity check fails on any rank.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 under
 torch.distributed.run (one process per GPU).
@@ -77,7 +82,8 @@ VARIANTS = {0: "ahead-of-time kernels (runtime geometry) for every launch",
             1: "ahead-of-time kernels for the replicas (throughput launches); the configuration compiled into "
                "the kernel (jit.cpp) for one simulation alone (latency launches)",
             2: "configuration compiled into the kernel (jit.cpp) for every launch"}
-COMPILERS = {1: "hipRTC at run time", 2: "hipcc at build time"}
+COMPILERS = {1: "hipRTC at run time", 2: "hipcc at build time",
+             3: "throughput and latency code objects from different compilers (hipcc / hipRTC)"}
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 SEED_BASE = 4
 STAGE_GROUP = 256       # replicas whose requests the host generates per staging copy
@@ -203,7 +209,7 @@ def cpu_baseline(cfg_xml: str, cfg, reqs: np.ndarray, threads, fill: int, budget
 
 
 # ---------------------------------------------------------------- CPU ensemble
-def _ensemble_worker(conn, cfg_xml: str, fill: int, n_timed: int, budget_s: float) -> None:
+def _ensemble_worker(conn, cfg_xml: str, fill: int, n_timed: int, budget_s: float, rank: int = 0) -> None:
     """One replica of the ensemble: wait for its replica index (the parent
     knows the replica count only once it has the GPU), fill untimed, wait for
     "go", run for budget_s; send back every delay it produced (parity)."""
@@ -215,7 +221,7 @@ def _ensemble_worker(conn, cfg_xml: str, fill: int, n_timed: int, budget_s: floa
         import primesim_amd as P
         from primesim_amd.dist import replica_seed
         cfg = P.load_config(cfg_xml)
-        reqs = P.generate_stream(stream_spec(replica_seed(SEED_BASE, 0, rep), fill + n_timed))
+        reqs = P.generate_stream(stream_spec(replica_seed(SEED_BASE, rank, rep), fill + n_timed))
         threads = P.stream_threads(stream_spec(SEED_BASE))
         kind, eng = reference_engine(cfg_xml, cfg)
         for prog, th in threads:
@@ -269,15 +275,15 @@ class Ensemble:
     while the GPU warms up, and returns its delays: the parity check of those
     replicas against the GPU's."""
 
-    def __init__(self, cfg_xml: str, workers: int, fill: int, n_timed: int, budget_s: float):
+    def __init__(self, cfg_xml: str, workers: int, fill: int, n_timed: int, budget_s: float, rank: int = 0):
         ctx = mp.get_context("fork")
-        self.workers, self.budget = workers, budget_s
+        self.workers, self.budget, self.rank = workers, budget_s, rank
         self.fill = fill
         self.pipes, self.procs = [], []
         self.replicas: list = []
         for w in range(workers):
             a, b = ctx.Pipe()
-            p = ctx.Process(target=_ensemble_worker, args=(b, cfg_xml, fill, n_timed, budget_s), daemon=True)
+            p = ctx.Process(target=_ensemble_worker, args=(b, cfg_xml, fill, n_timed, budget_s, rank), daemon=True)
             p.start()
             self.pipes.append(a)
             self.procs.append(p)
@@ -321,6 +327,43 @@ class Ensemble:
                           f"over the GPU's replicas) after an untimed {self.fill}-request fill, run concurrently for "
                           f"{self.budget:g} s: {n} requests in {el:.2f} s (wall {wall:.2f} s)",
                 "per_process_accesses_per_s": [r[1] / r[2] for r in res]}
+
+
+def replica_parity(ens: Ensemble, H, slots: int, kind: str, warm_reqs: int) -> dict:
+    """The GPU delays of the ensemble's replicas (warmup, then timed window)
+    against the reference's on the same streams, over the requests both ran."""
+    per = {}
+    for r, d_cpu in ens.delays.items():
+        g = H.kept[r]
+        m = min(len(g), len(d_cpu))
+        per[str(r)] = {"requests_compared": m, "gpu_window_requests": int(H.adv[r]),
+                       "spare": bool(r >= slots),
+                       "bit_identical": bool(np.array_equal(g[:m], d_cpu[:m]))}
+    # spares the pool started mid-slice and that ran requests of the timed window
+    spares_run = [int(k) for k, v in per.items() if v["spare"] and v["gpu_window_requests"] > 0]
+    return {"replicas": sorted(ens.delays), "count": len(per),
+            "requests_compared": sum(v["requests_compared"] for v in per.values()),
+            "bit_identical": all(v["bit_identical"] for v in per.values()),
+            "spares_started_and_compared": spares_run,
+            "covers_pool_handoff": bool(H.pool) and len(spares_run) > 0,
+            "per_replica": per,
+            "note": f"GPU delays of each replica (its {warm_reqs}-request warmup, then its timed window) against "
+                    f"the {kind} uncore's on the same stream, run by the ensemble processes, compared over the "
+                    f"requests both ran"}
+
+
+def job_roofline(infos: list) -> dict:
+    """The whole job's roofline: algorithmic bytes per launch summed over the
+    ranks / the slowest rank's mean launch time / (ranks x HBM peak)."""
+    n = len(infos)
+    b = sum(i["bytes_per_launch"] for i in infos)
+    ms = max(i["avg_launch_ms"] for i in infos)
+    ach = b / (ms / 1e3) / 1e9
+    return {"achieved": ach, "peak": n * HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / (n * HBM_PEAK_GBS),
+            "alg_bytes_per_launch": b, "avg_launch_ms_max_over_ranks": ms,
+            "per_rank_frac": [i["bytes_per_launch"] / (i["avg_launch_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS for i in infos],
+            "note": f"algorithmic bytes per launch summed over {n} rank(s) / the max over ranks of the HIP-event mean "
+                    f"launch time / ({n} x {HBM_PEAK_GBS:g} GB/s)"}
 
 
 # ---------------------------------------------------------------- GPU passes
@@ -409,27 +452,31 @@ def run_pass(um, args, R: int, rank: int, world: int, dev, stream, replay: int, 
     # HIP events on the engine's (non-null) stream time exactly its launches
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     um.set_device_req_format(P.uncore.PU_REQ_FMT_16 if rb == 16 else P.uncore.PU_REQ_FMT_32)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(steps):
-        ev[k][0].record(stream)
-        if pool:
-            um.run_device_pool(d_win.data_ptr(), d_win_off.data_ptr(), d_win_delay.data_ptr(), d_pos.data_ptr(),
-                               d_sched.data_ptr(), slots, int(args.slice_ms * 1000), sptr)
-        elif args.slice_ms > 0:
-            um.run_device_sliced(d_win.data_ptr(), d_win_off.data_ptr(), d_win_delay.data_ptr(), d_pos.data_ptr(),
-                                 int(args.slice_ms * 1000), sptr)
-        else:
-            um.run_device_sliced(d_win.data_ptr(), step_offs[k].data_ptr(), d_win_delay.data_ptr(), d_pos.data_ptr(),
-                                 0, sptr)
-        ev[k][1].record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    um.set_device_req_format(P.uncore.PU_REQ_FMT_32)
+    try:
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(steps):
+            ev[k][0].record(stream)
+            if pool:
+                um.run_device_pool(d_win.data_ptr(), d_win_off.data_ptr(), d_win_delay.data_ptr(), d_pos.data_ptr(),
+                                   d_sched.data_ptr(), slots, int(args.slice_ms * 1000), sptr)
+            elif args.slice_ms > 0:
+                um.run_device_sliced(d_win.data_ptr(), d_win_off.data_ptr(), d_win_delay.data_ptr(),
+                                     d_pos.data_ptr(), int(args.slice_ms * 1000), sptr)
+            else:
+                um.run_device_sliced(d_win.data_ptr(), step_offs[k].data_ptr(), d_win_delay.data_ptr(),
+                                     d_pos.data_ptr(), 0, sptr)
+            ev[k][1].record(stream)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+    finally:
+        # the 32-B records the warm-up chunks (and any later pass) use, even
+        # when a launch or the barrier raised
+        um.set_device_req_format(P.uncore.PU_REQ_FMT_32)
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     log(f"[bench] timed {steps} steps in {elapsed:.3f}s; per-launch ms {['%.1f' % x for x in kern_ms]}")
     pos = d_pos.cpu().numpy().view(np.uint64)
@@ -577,6 +624,10 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--ensemble-seconds", type=float, default=3.0)
     ap.add_argument("--ensemble-workers", type=int, default=0, help="0 = every host core of this job's share")
+    ap.add_argument("--rank-parity-workers", type=int, default=2,
+                    help="N > 1: reference processes per rank (forked before the GPU) replaying that rank's replica 0 "
+                         "and its first pool spare; their delays are checked against the GPU's and gathered to rank 0 "
+                         "(0 = no parity at N > 1)")
     ap.add_argument("--closed-steps", type=int, default=5, help="timed steps of the closed-loop pass (0 = skip)")
     ap.add_argument("--single-requests", type=int, default=40960)
     ap.add_argument("--no-cpu", action="store_true")
@@ -659,7 +710,7 @@ def main(argv=None) -> None:
     import primesim_amd as P
     from primesim_amd import _abi as A
     from primesim_amd import config as CF
-    from primesim_amd.dist import reduce_run, replica_seed
+    from primesim_amd.dist import gather_objects, reduce_run, replica_seed
 
     sim = CF.preset("C4")
     xml_path = os.path.join(tempfile.gettempdir(), f"pu_bench_c4_{os.getpid()}.xml")
@@ -667,11 +718,15 @@ def main(argv=None) -> None:
     cfg = P.load_config(xml_path)
     threads = P.stream_threads(stream_spec(SEED_BASE))
 
-    # ---- the CPU ensemble forks now, before this process touches the GPU
+    # ---- the CPU ensemble forks now, before this process touches the GPU: at
+    # N=1 one reference process per host core (parity + the ensemble baseline);
+    # at N>1 a few per rank, replaying this rank's replica 0 and first pool
+    # spare (parity of every rank's line)
     ens = None
-    if extras and not args.no_cpu:
-        nw = args.ensemble_workers or host_core_share()
-        ens = Ensemble(xml_path, nw, args.warmup * args.chunk, args.steps * args.chunk, args.ensemble_seconds)
+    rank_parity = world > 1 and not args.no_cpu and args.rank_parity_workers > 0
+    if (extras and not args.no_cpu) or rank_parity:
+        nw = (args.ensemble_workers or host_core_share()) if extras else args.rank_parity_workers
+        ens = Ensemble(xml_path, nw, args.warmup * args.chunk, args.steps * args.chunk, args.ensemble_seconds, rank)
 
     import torch.distributed as dist
     if world > 1:
@@ -684,7 +739,7 @@ def main(argv=None) -> None:
     LAST_REPLICAS = R
     # the ensemble's replicas, spread over 0..R-1: their delays are checked
     # against the reference's bit for bit (replica 0 also by cpu_baseline)
-    keep = sorted(set(ens.assign(R, D.slots)) | {0}) if ens is not None else ([0] if rank == 0 else [])
+    keep = sorted(set(ens.assign(R, D.slots)) | {0}) if ens is not None else [0]
 
     # ---- headline: open-loop replay
     H = D.headline(args, rank, world, keep)
@@ -702,34 +757,38 @@ def main(argv=None) -> None:
     busy_err = busy_guard(H.pool)
     if busy_err:
         log(f"[bench] {busy_err}")
+    # every rank: its replicas' parity against the reference, then the gather
+    ens_res, rparity = None, None
+    if ens is not None:
+        ens_res = ens.run()
+        log(f"[bench] rank {rank}: cpu ensemble ({ens_res['kind']}, {ens_res['cores']} processes): "
+            f"{ens_res['value']:.0f} accesses/s")
+        rparity = replica_parity(ens, H, D.slots, ens_res["kind"], args.warmup * args.chunk)
+        log(f"[bench] rank {rank}: replica parity: {rparity['count']} replicas "
+            f"({rparity['replicas'][0]}..{rparity['replicas'][-1]}), "
+            f"{rparity['requests_compared']} delays, bit-identical {rparity['bit_identical']}")
+    infos = gather_objects({"rank": rank, "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_ms,
+                            "replicas": R, "wavefronts": D.slots,
+                            "parity": None if rparity is None else
+                            {k: rparity[k] for k in ("replicas", "requests_compared", "bit_identical",
+                                                     "covers_pool_handoff", "spares_started_and_compared")}})
+    ranks_checked = [i for i in infos if i["parity"] is not None]
+    ranks_parity = None
+    if world > 1 and ranks_checked:
+        ranks_parity = {"bit_identical": all(i["parity"]["bit_identical"] for i in ranks_checked),
+                        "ranks_checked": len(ranks_checked),
+                        "requests_compared": sum(i["parity"]["requests_compared"] for i in ranks_checked),
+                        "per_rank": [{"rank": i["rank"], **i["parity"]} for i in infos if i["parity"] is not None],
+                        "note": "each rank replays its replica 0 and its first replica-pool spare (or its last replica "
+                                "without a pool) on the reference uncore in processes forked before the GPU; their "
+                                "delays (warmup and timed window) are compared with that rank's GPU delays over the "
+                                "requests both ran, then gathered to rank 0"}
+        parity_ok &= ranks_parity["bit_identical"]
+    if rparity is not None:
+        parity_ok &= rparity["bit_identical"]
+    job_rf = job_roofline(infos)
     if rank == 0:
-        ens_res = ens.run() if ens is not None else None
-        replica_parity = None
-        if ens_res:
-            log(f"[bench] cpu ensemble ({ens_res['kind']}, {ens_res['cores']} processes): "
-                f"{ens_res['value']:.0f} accesses/s")
-            per = {}
-            for r, d_cpu in ens.delays.items():
-                g = H.kept[r]
-                m = min(len(g), len(d_cpu))
-                per[str(r)] = {"requests_compared": m, "gpu_window_requests": int(H.adv[r]),
-                               "spare": bool(r >= D.slots),
-                               "bit_identical": bool(np.array_equal(g[:m], d_cpu[:m]))}
-            # spares the pool started mid-slice and that ran requests of the timed window
-            spares_run = [int(k) for k, v in per.items() if v["spare"] and v["gpu_window_requests"] > 0]
-            replica_parity = {"replicas": sorted(ens.delays), "count": len(per),
-                              "requests_compared": sum(v["requests_compared"] for v in per.values()),
-                              "bit_identical": all(v["bit_identical"] for v in per.values()),
-                              "spares_started_and_compared": spares_run,
-                              "covers_pool_handoff": bool(H.pool) and len(spares_run) > 0,
-                              "per_replica": per,
-                              "note": f"GPU delays of each replica (its {args.warmup * args.chunk}-request warmup, "
-                                      f"then its timed window) against the {ens_res['kind']} uncore's on the same "
-                                      f"stream, run by the ensemble processes, compared over the requests both ran"}
-            parity_ok &= replica_parity["bit_identical"]
-            log(f"[bench] replica parity: {replica_parity['count']} replicas "
-                f"({replica_parity['replicas'][0]}..{replica_parity['replicas'][-1]}), "
-                f"{replica_parity['requests_compared']} delays, bit-identical {replica_parity['bit_identical']}")
+        replica_parity_res = rparity if world == 1 else None
         closed = None
         if extras and args.closed_steps > 0:
             um.reset()
@@ -865,11 +924,14 @@ def main(argv=None) -> None:
                 "avg_launch_ms": avg_ms,
                 "alg_bytes_per_launch": bytes_per_launch,
                 "limiter": LIMITER,
+                "scope": "rank 0's kernel: its algorithmic bytes per launch / its HIP-event mean launch time",
+                "job": job_rf,
             },
             "cpu_baseline": cpu,
-            "cpu_baseline_ensemble": ens_res,
-            "replica_parity": replica_parity,
-            "parity": parity_ok if (not args.no_cpu and world == 1) else None,
+            "cpu_baseline_ensemble": ens_res if world == 1 else None,
+            "replica_parity": replica_parity_res,
+            "rank_parity": ranks_parity,
+            "parity": parity_ok if (not args.no_cpu and (world == 1 or ranks_parity is not None)) else None,
             "busy_guard": busy_err or f"ok: replica-pool busy fraction >= {BUSY_MIN} (or the pool ran dry)",
         }
         print(json.dumps(result), flush=True)

@@ -268,9 +268,11 @@ long pu_config_geo_source(const pu_sim_cfg* cfg, char* buf, size_t cap);
  * headers in LDS) and the ahead-of-time kernels for throughput launches
  * (PRIMEUNCORE_JIT_THROUGHPUT=0; sets wider than 64 ways always take 2);
  * 0 the ahead-of-time kernels only.  pu_compiled_compiler tells which
- * compiler built the throughput code object handle h runs: 2 hipcc (written
- * by pu_config_jit_warm in a process that has not used the GPU, the
- * build-time warm-up), 1 hipRTC (a cache miss at run time), 0 none. */
+ * compiler built the two code objects (throughput and latency kernels) handle
+ * h runs: 2 hipcc for both (written by pu_config_jit_warm in a process that
+ * set PRIMEUNCORE_JIT_OFFLINE=1 and has not used the GPU: the build-time
+ * warm-up, tools/jit_warm.py), 1 hipRTC for both (cache misses at run time),
+ * 3 one of each, 0 none. */
 int pu_config_jit_warm(const pu_sim_cfg* cfg);
 int pu_compiled_config(const pu_handle* h);
 int pu_compiled_compiler(const pu_handle* h);

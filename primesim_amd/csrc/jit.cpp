@@ -36,6 +36,7 @@
 
 #include <atomic>
 #include <cerrno>
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -221,10 +222,46 @@ std::string offline_cc() {
     return ::access(p.c_str(), X_OK) == 0 ? p : "";
 }
 
-// Set once this process has loaded engine code on the GPU (jit_load): from
-// then on nothing is compiled by starting another program, only by hipRTC
-// in-process (a process that has initialised the GPU starts no compiler).
+// Set once this library touches HIP (pu_create, the unit hooks, jit_load,
+// device_arch): from then on nothing is compiled by starting another program,
+// only by hipRTC in-process (a process that has initialised the GPU starts no
+// compiler).  The library cannot see HIP use by others in the process (torch,
+// another library), so the offline compiler is also opt-in: only a process
+// that sets PRIMEUNCORE_JIT_OFFLINE=1 (tools/jit_warm.py, which never touches
+// the GPU) starts it.
 std::atomic<bool> g_gpu_used{false};
+bool offline_allowed() {
+    const char* e = std::getenv("PRIMEUNCORE_JIT_OFFLINE");
+    return e && e[0] == '1' && !g_gpu_used;
+}
+
+// The offline compiler's identity for the cache key: the resolved driver and
+// clang paths with their size and modification time, and the ROCm version
+// file — no child process (jit_key also runs in processes that use the GPU).
+const std::string& offline_cc_identity() {
+    static const std::string id = [] {
+        std::string s;
+        auto add = [&](const std::string& path) {
+            char rp[PATH_MAX];
+            struct stat st;
+            if (path.empty() || !::realpath(path.c_str(), rp) || ::stat(rp, &st) != 0) {
+                s += "|-";
+                return;
+            }
+            s += std::string("|") + rp + ":" + std::to_string((long long)st.st_size) + ":" +
+                 std::to_string((long long)st.st_mtime);
+        };
+        const std::string cc = offline_cc();
+        add(cc);
+        const char* r = std::getenv("ROCM_PATH");
+        const std::string root = r && *r ? r : "/opt/rocm";
+        add(root + "/lib/llvm/bin/clang");
+        std::vector<char> v;
+        if (read_file(root + "/.info/version", &v)) s += "|" + std::string(v.begin(), v.end());
+        return s;
+    }();
+    return id;
+}
 
 // Compile with the offline compiler (a child process, never from a process
 // that has initialised the GPU): the embedded sources and the configuration
@@ -313,6 +350,8 @@ std::string jit_source_tag() {
     return buf;
 }
 
+void jit_note_gpu() { g_gpu_used = true; }
+
 std::string jit_key(const Geo& g, int waves_1level, const std::string& arch, int part, int cc) {
     uint64_t h = fnv1a("primeuncore-jit-2");
     for (int i = 0; i < pu_jit_nsrc; i++) {
@@ -324,6 +363,7 @@ std::string jit_key(const Geo& g, int waves_1level, const std::string& arch, int
     int maj = 0, min = 0;
     hiprtcVersion(&maj, &min);
     h = fnv1a(std::to_string(maj) + "." + std::to_string(min), h);
+    if (cc == kJitOffline) h = fnv1a(offline_cc_identity(), h);   // a different or upgraded hipcc/clang
     char buf[17];
     std::snprintf(buf, sizeof buf, "%016llx", (unsigned long long)h);
     return jit_source_tag() + "-" + buf;
@@ -337,6 +377,7 @@ int jit_waves() {
 
 // The current device's target ("gfx950" from "gfx950:sramecc+:xnack-").
 std::string device_arch() {
+    g_gpu_used = true;
     int dev = 0;
     hipDeviceProp_t p;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return kBuildArch;
@@ -426,10 +467,10 @@ bool load_part(const Geo& g, int waves, const std::string& arch, int part, JitKe
 
 int jit_load(const Geo& g, JitKernels* out, bool verbose) {
     *out = JitKernels{};
+    g_gpu_used = true;
     if (!jit_enabled()) return 0;
     const int waves = jit_waves();
     const std::string arch = device_arch();
-    g_gpu_used = true;
     std::lock_guard<std::mutex> lk(g_jit_mu);   // one compile at a time; another thread may have built it
     std::string key[kJitParts];
     for (int part = 0; part < kJitParts; part++)
@@ -448,7 +489,7 @@ int jit_warm(const Geo& g, std::string* key_out) {
     const int waves = jit_waves();
     // the offline compiler when present (and this process has put nothing on
     // the GPU), else hipRTC; a part already cached under either is kept
-    const bool offline = !g_gpu_used && !offline_cc().empty();
+    const bool offline = offline_allowed() && !offline_cc().empty();
     std::lock_guard<std::mutex> lk(g_jit_mu);
     int cached = 0;
     for (int part = 0; part < kJitParts; part++) {

@@ -28,6 +28,8 @@ struct JitKernels {
 };
 
 bool jit_enabled();
+// The library is about to touch HIP: from now on no compiler process is started.
+void jit_note_gpu();
 std::string jit_source_tag();
 std::string jit_key(const Geo& g, int waves_1level, const std::string& arch, int part, int cc);
 // Load (compiling on a cache miss) the kernels of configuration g; leaves

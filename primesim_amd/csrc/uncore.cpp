@@ -538,7 +538,10 @@ int pu_config_jit_warm(const pu_sim_cfg* cfg) {
 
 int pu_compiled_config(const pu_handle* h) { return h && h->jit.ok ? (h->jit_throughput ? 2 : 1) : 0; }
 int pu_compiled_compiler(const pu_handle* h) {
-    return h && h->jit.ok ? (h->jit.cc[0] == pu::kJitOffline ? 2 : 1) : 0;
+    if (!h || !h->jit.ok) return 0;
+    int off = 0;
+    for (int part = 0; part < pu::kJitParts; part++) off += h->jit.cc[part] == pu::kJitOffline;
+    return off == pu::kJitParts ? 2 : off == 0 ? 1 : 3;   // 3: the parts came from different compilers
 }
 
 const char* pu_jit_source_tag(void) {
@@ -577,6 +580,7 @@ pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device) {
     }
     Geo geo;
     if (build_geo(cfg, &geo) != 0) return nullptr;
+    pu::jit_note_gpu();   // this process starts no compiler from here on
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) {
         pu::set_error(PU_ENODEV, "no HIP device available (the engine has no CPU fallback)");
@@ -682,16 +686,24 @@ uint64_t pu_replica_pool_bytes(const pu_handle* h) {
 }
 
 namespace pu {
+// The device's target name ("gfx950" from "gfx950:sramecc+:xnack-").
+std::string device_target(int device) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, device) != hipSuccess) return "";
+    const std::string a = p.gcnArchName;
+    return a.substr(0, a.find(':'));
+}
 // gfx950 hands LDS to workgroups in 1,280-B units out of a CU's 160 KB
 // (measured: tools/probe/residency.hip, profiles/r5a_residency.json — one-wave
 // workgroups of 6,144 / 7,152 / 8,192 / 16,384 / 32,768 B reside 25 / 21 /
 // 18 / 9 / 4 per CU, hipOccupancy says 26 / 22 / 20 / 10 / 5).  A time-sliced
 // launch whose grid exceeds the resident waves takes two slices: round 4's
 // six-wave kernel (7,152 B: 22 by hipOccupancy, 21 resident) ran at half rate.
+// Other targets are not measured: their residency is hipOccupancy's alone.
 constexpr int kLdsGranule = 1280;
-int lds_limited_per_cu(int lds_bytes, int lds_per_cu) {
-    if (lds_bytes <= 0) return 1 << 30;
-    const int unit = (lds_bytes + kLdsGranule - 1) / kLdsGranule * kLdsGranule;
+int lds_limited_per_cu(int lds_bytes, int lds_per_cu, int granule) {
+    if (lds_bytes <= 0 || lds_per_cu <= 0 || granule <= 0) return 1 << 30;
+    const int unit = (lds_bytes + granule - 1) / granule * granule;
     return lds_per_cu / unit;
 }
 }  // namespace pu
@@ -700,7 +712,11 @@ int pu_resident_replicas(const pu_handle* h) {
     if (!h) return pu::set_error(PU_EINVAL, "null handle");
     int cus = 0, lds_cu = 0, per_cu = 1 << 30;
     HIP_TRY(hipSetDevice(h->device), PU_ENODEV);
-    HIP_TRY(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, h->device), PU_EIO);
+    // a device that reports no per-CU LDS (0, or a per-block figure below one
+    // workgroup's) keeps hipOccupancy's count rather than resolving to 0 slots
+    if (hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, h->device) != hipSuccess)
+        lds_cu = 0;
+    const int granule = pu::device_target(h->device) == "gfx950" ? pu::kLdsGranule : 0;
     // both throughput launch kinds (time-sliced, replica pool: separate
     // instantiations, each its own registers and LDS), one wave per replica
     for (int mode = 1; mode <= 2; mode++) {
@@ -708,7 +724,8 @@ int pu_resident_replicas(const pu_handle* h) {
         int rc = h->jit.ok && h->jit_throughput ? pu::jit_occupancy(h->jit, mode, &n, &lds)
                                                 : pu_engine_occupancy(h->geo.num_levels, mode, &n, &lds);
         if (rc) return pu::set_error(rc, "occupancy query failed");
-        n = std::min(n, pu::lds_limited_per_cu(lds, lds_cu));
+        const int by_lds = pu::lds_limited_per_cu(lds, lds_cu, granule);
+        if (by_lds > 0) n = std::min(n, by_lds);
         per_cu = std::min(per_cu, n);
     }
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device), PU_EIO);
@@ -1226,6 +1243,7 @@ struct DevBufs {
 };
 
 int unit_prepare(int device) {
+    pu::jit_note_gpu();
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev)
         return pu::set_error(PU_ENODEV, "no HIP device available");

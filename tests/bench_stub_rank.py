@@ -7,6 +7,8 @@ restatement of the uncore (oracle.CpuRef, standing in for one GPU's engine:
 the same replica seeds, the same C4 stream, a fixed number of requests each),
 and bench reduces the timing / request counts and prints the JSON line
 exactly as on GPUs.  Rank r reports an elapsed time of 0.5 + r seconds.
+PU_STUB_CORRUPT_RANK=k changes one delay of rank k's last kept replica (the
+per-rank parity must catch it).
 """
 import os
 import sys
@@ -42,7 +44,8 @@ class StubDevice:
         import oracle as O
         import primesim_amd as P
         from primesim_amd.dist import replica_seed
-        delta, rep0, processed = {}, [], 0
+        delta, rep0, processed, kept = {}, [], 0, {}
+        corrupt = os.environ.get("PU_STUB_CORRUPT_RANK")
         for r in range(self.R):
             reqs = P.generate_stream(bench.stream_spec(replica_seed(bench.SEED_BASE, rank, r), REQS_PER_REPLICA))
             eng = O.CpuRef(self.cfg)
@@ -52,6 +55,10 @@ class StubDevice:
             assert rc == 0
             if r == 0:
                 rep0.append(d)
+            if r in keep:
+                kept[r] = d.copy()
+                if corrupt is not None and int(corrupt) == rank and r == max(keep):
+                    kept[r][len(d) // 2] += 1          # one wrong delay on this rank's last kept replica
             for k, v in eng.stats().as_dict().items():
                 if k not in ("error_flags", "num_levels"):
                     delta[k] = delta.get(k, 0) + v
@@ -59,7 +66,7 @@ class StubDevice:
         with open(os.path.join(os.environ["PU_STUB_OUT"], f"rank{rank}.txt"), "w") as f:
             f.write(f"{processed} {int(sum(int(x.astype(np.int64).sum()) for x in rep0))}\n")
         return bench.Pass(elapsed=0.5 + rank, kern_ms=[1.0] * args.steps, adv=np.array([REQS_PER_REPLICA] * self.R),
-                          kept={0: rep0[0]}, delta=delta, halted=0, errf=0, per_replica=None, steps=args.steps,
+                          kept=kept, delta=delta, halted=0, errf=0, per_replica=None, steps=args.steps,
                           processed=processed, pool=None)
 
     def reduce_device(self, args):

@@ -40,6 +40,48 @@ def test_two_ranks_launched_by_bench_reduce_over_ranks(tmp_path):
     assert b["per_simulation_accesses_per_s"] == b["value"] / 4
     assert per_rank[0][1] != per_rank[1][1]      # the ranks simulated disjoint replicas (seeds)
     assert b["parity"] is None and b["cpu_baseline"] is None   # the CPU baseline is an N=1 line only
+    assert b["rank_parity"] is None                              # --no-cpu: no reference processes
+    job = b["roofline"]["job"]
+    assert job["peak"] == 2 * bench_peak() and len(job["per_rank_frac"]) == 2
+    assert job["avg_launch_ms_max_over_ranks"] == 1.0
+
+
+def bench_peak():
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.HBM_PEAK_GBS
+
+
+# the stub's ranks run 1,200 requests per replica: the reference processes
+# fill 600 (the "warmup") and replay the next 600 (the "timed window")
+PARITY_ARGS = ["--gpus", "2", "--dist-backend", "gloo", "--steps", "1", "--warmup", "1", "--chunk", "600",
+               "--ensemble-seconds", "2"]
+
+
+def test_two_ranks_check_their_replicas_against_the_reference(tmp_path):
+    """N>1: each rank forks reference processes for two of its replicas,
+    compares their delays with its own and the results are gathered: the line
+    carries parity true, one entry per rank, and the job-level roofline."""
+    r = _run(PARITY_ARGS, tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    b = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    rp = b["rank_parity"]
+    assert b["parity"] is True and rp["bit_identical"] is True
+    assert [p["rank"] for p in rp["per_rank"]] == [0, 1]
+    for p in rp["per_rank"]:
+        assert p["replicas"] == [0, 1] and p["bit_identical"]
+        assert p["requests_compared"] == 2 * 1200
+    assert b["cpu_baseline_ensemble"] is None and b["replica_parity"] is None
+
+
+def test_a_mismatch_on_one_rank_fails_the_job(tmp_path):
+    r = _run(PARITY_ARGS, tmp_path, {"PU_STUB_CORRUPT_RANK": "1"})
+    assert r.returncode == 1, r.stderr[-3000:]
+    b = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    rp = b["rank_parity"]
+    assert b["parity"] is False and rp["bit_identical"] is False
+    assert [p["bit_identical"] for p in rp["per_rank"]] == [True, False]
+    assert "PARITY FAILURE" in r.stderr
 
 
 def test_gpus_must_match_world_size(tmp_path):

@@ -18,7 +18,8 @@ CODE = ("import ctypes as C, sys; sys.path.insert(0, %r); import primesim_amd as
 
 
 def _warm(cache, **env):
-    e = dict(os.environ, PRIMEUNCORE_JIT_CACHE=str(cache), **env)
+    e = dict(os.environ, PRIMEUNCORE_JIT_CACHE=str(cache), PRIMEUNCORE_JIT_OFFLINE="1")
+    e.update(env)
     r = subprocess.run([sys.executable, "-c", CODE], env=e, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     return int(r.stdout.strip().splitlines()[-1])
@@ -40,3 +41,8 @@ def test_warm_up_compiles_both_parts_with_either_compiler(tmp_path):
         assert len(thr) == 1 and len(lat) == 1 and thr[0] is not lat[0]
         assert b"pu_jit_uncore_s1_h1" not in thr[0] and b"pu_jit_uncore_s2_h0" not in lat[0]
     assert _warm(off) == 1                                   # cached
+    # without the opt-in the warm-up never starts hipcc: hipRTC's objects
+    rtc2 = tmp_path / "no_opt_in"
+    rtc2.mkdir()
+    assert _warm(rtc2, PRIMEUNCORE_JIT_OFFLINE="0") == 0
+    assert sorted(p.name for p in rtc2.glob("*.hsaco")) == fr

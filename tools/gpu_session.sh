@@ -16,6 +16,7 @@
 #   sq_single    the same for one simulation alone, open loop and closed loop (latency kernel)
 #   handoff      tools/probe/handoff: dependent hand-off latency between two waves
 #   tworank      bench.py --gpus 2 with both ranks on card 0 (gloo)
+#   tworank_parity  the same with each rank's reference parity processes and the job-level roofline
 #   regions_single  lone-wave region profiles of the shipped compiled-configuration latency kernel
 #                (-DPU_PROF through PRIMEUNCORE_JIT_EXTRA), open and closed loop
 #   regions_ens  the same for the throughput kernel at the headline's replica count
@@ -83,6 +84,7 @@ for S in "$@"; do
                timeout -k 10 500 python tools/pmc_sq.py --kernel pu_jit_uncore_s1_h1 --work /tmp/pmc_sq2 --out ${O}_sq_single_closed.json -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras --replay closed > ${O}_sq_single_closed.log 2>&1 || exit 1;;
     handoff) timeout -k 10 120 tools/probe/handoff > ${O}_handoff.json 2> ${O}_handoff.log || exit 1;;
     tworank) PU_BENCH_DEVICE=0 timeout -k 10 300 $BENCH --gpus 2 --steps 3 --warmup 2 --no-cpu --dist-backend gloo > ${O}_two_rank.json 2> ${O}_two_rank.log || exit 1;;
+    tworank_parity) PU_BENCH_DEVICE=0 timeout -k 10 400 $BENCH --gpus 2 --steps 3 --warmup 2 --dist-backend gloo > ${O}_two_rank_parity.json 2> ${O}_two_rank_parity.log || exit 1;;
     regions_single)
       timeout -k 10 200 python tools/prof_regions.py --jit -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras > ${O}_regions_single_open.txt 2>&1 || exit 1
       timeout -k 10 200 python tools/prof_regions.py --jit -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras --replay closed > ${O}_regions_single_closed.txt 2>&1 || exit 1;;

@@ -23,6 +23,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PRUNE_HOURS = 1   # grace for code objects written by a library being rebuilt
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+# this process and its workers never touch the GPU: the library may start the
+# offline compiler (hipcc) here, and only here (jit.cpp offline_allowed)
+os.environ["PRIMEUNCORE_JIT_OFFLINE"] = "1"
 
 
 def configs():
