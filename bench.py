@@ -74,6 +74,26 @@ LAUNCH_CMD = None       # rank command for launch_ranks (None: this file; tests 
 LAST_REPLICAS = 0       # replicas of the last main() run (tools/prof_regions.py)
 LAST_PER_REPLICA = None  # per-replica stat deltas of the timed steps (profiling runs only)
 METRIC = "simulated memory accesses/sec (uncore) at 1024 cores; % HBM roofline"
+# --config: the SURVEY.md §8d shape and its seeded stream.  C4 is the metric's
+# configuration (BASELINE.json configs[3]); C3 and C5 are the deeper and the
+# larger shapes, measured the same way (their lines name their own metric).
+WORKLOADS = {
+    "C3": {"cores": 256, "stream": "PU_STREAM_MULTIPROGRAM", "num_progs": 4, "replay": "open",
+           "desc": "C3: 256-core 16x16 mesh, private L1 32KB/8W + private L2 256KB/8W/5cyc + 1MB/16W shared-LLC "
+                   "slice per tile, directory MESI full-map; multi-programmed mix, 4 programs x 64 cores, "
+                   "per-program footprints 4-64 MB, 20% writes"},
+    "C4": {"cores": 1024, "stream": "PU_STREAM_UNIFORM_HOTSPOT", "num_progs": 1, "replay": "open",
+           "desc": "C4: 1024-core 32x32 mesh, L1 32KB/8W + 256KB/8W shared-LLC slice per tile, "
+                   "directory MESI full-map, uniform 2^20 lines + 64-line hotspot, 25% writes"},
+    # open loop, the producer/consumer stream's link delays pass 2^31 within
+    # its first quantum (golden big_c5_preset stops at request 165,860 by
+    # prime.cpp:130-134): every replica would halt in the warm-up, so C5 is
+    # replayed closed loop (core_manager.cpp:265) by default
+    "C5": {"cores": 4096, "stream": "PU_STREAM_PRODUCER_CONSUMER", "num_progs": 1, "replay": "closed",
+           "desc": "C5: 4096-core 64x64 mesh, L1 32KB/8W + 256KB/8W shared-LLC slice per tile, directory MESI "
+                   "full-map; producer/consumer pairs (p, p+2048) sharing 1,024-line buffers, 50% writes"},
+}
+WORKLOAD = "C4"         # set by main() before the ensemble forks (its workers read it)
 LIMITER = ("dependent-load latency and instruction issue (profiles/r5x_sq.json: 26% of wave cycles issuing, "
            "38% waiting on memory, 36% in issue stalls at 7 waves/SIMD; fabric traffic about 41% of 8 TB/s), "
            "not HBM bandwidth")
@@ -163,7 +183,9 @@ def host_core_share() -> int:
 def stream_spec(seed: int, n: int = 0):
     import primesim_amd as P
     from primesim_amd import _abi as A
-    return P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=seed, num_quanta=64, max_requests=n)
+    w = WORKLOADS[WORKLOAD]
+    return P.StreamSpec(getattr(A, w["stream"]), w["cores"], seed=seed, num_quanta=64, num_progs=w["num_progs"],
+                        max_requests=n)
 
 
 def reference_engine(cfg_xml: str, cfg, mode: int = 0):
@@ -175,6 +197,12 @@ def reference_engine(cfg_xml: str, cfg, mode: int = 0):
     eng = O.RefUncore(cfg_xml, plain=True) if kind == "reference" else O.CpuRef(cfg)
     eng.set_mode(mode)
     return kind, eng
+
+
+def ref_mode(args) -> int:
+    """The reference's replay mode for the headline's (oracle MODE_*)."""
+    import oracle as O
+    return O.MODE_CLOSED if args.replay == "closed" else 0
 
 
 def simulated(n: int, rc: int) -> int:
@@ -209,7 +237,8 @@ def cpu_baseline(cfg_xml: str, cfg, reqs: np.ndarray, threads, fill: int, budget
 
 
 # ---------------------------------------------------------------- CPU ensemble
-def _ensemble_worker(conn, cfg_xml: str, fill: int, n_timed: int, budget_s: float, rank: int = 0) -> None:
+def _ensemble_worker(conn, cfg_xml: str, fill: int, n_timed: int, budget_s: float, rank: int = 0,
+                     mode: int = 0) -> None:
     """One replica of the ensemble: wait for its replica index (the parent
     knows the replica count only once it has the GPU), fill untimed, wait for
     "go", run for budget_s; send back every delay it produced (parity)."""
@@ -223,7 +252,7 @@ def _ensemble_worker(conn, cfg_xml: str, fill: int, n_timed: int, budget_s: floa
         cfg = P.load_config(cfg_xml)
         reqs = P.generate_stream(stream_spec(replica_seed(SEED_BASE, rank, rep), fill + n_timed))
         threads = P.stream_threads(stream_spec(SEED_BASE))
-        kind, eng = reference_engine(cfg_xml, cfg)
+        kind, eng = reference_engine(cfg_xml, cfg, mode)
         for prog, th in threads:
             eng.alloc_core(prog, th)
         delays = []
@@ -275,7 +304,8 @@ class Ensemble:
     while the GPU warms up, and returns its delays: the parity check of those
     replicas against the GPU's."""
 
-    def __init__(self, cfg_xml: str, workers: int, fill: int, n_timed: int, budget_s: float, rank: int = 0):
+    def __init__(self, cfg_xml: str, workers: int, fill: int, n_timed: int, budget_s: float, rank: int = 0,
+                 mode: int = 0):
         ctx = mp.get_context("fork")
         self.workers, self.budget, self.rank = workers, budget_s, rank
         self.fill = fill
@@ -283,7 +313,8 @@ class Ensemble:
         self.replicas: list = []
         for w in range(workers):
             a, b = ctx.Pipe()
-            p = ctx.Process(target=_ensemble_worker, args=(b, cfg_xml, fill, n_timed, budget_s, rank), daemon=True)
+            p = ctx.Process(target=_ensemble_worker, args=(b, cfg_xml, fill, n_timed, budget_s, rank, mode),
+                            daemon=True)
             p.start()
             self.pipes.append(a)
             self.procs.append(p)
@@ -323,7 +354,7 @@ class Ensemble:
                 "cpu_model": cpu_model(),
                 "sample": f"{nw} processes, one per host core of this job's share, each the "
                           f"{'reference uncore compiled from /root/reference/src, no counting wraps' if kind == 'reference' else kind} "
-                          f"on one GPU replica's C4 stream (replicas {self.replicas[0]}..{self.replicas[-1]}, spread "
+                          f"on one GPU replica's {WORKLOAD} stream (replicas {self.replicas[0]}..{self.replicas[-1]}, spread "
                           f"over the GPU's replicas) after an untimed {self.fill}-request fill, run concurrently for "
                           f"{self.budget:g} s: {n} requests in {el:.2f} s (wall {wall:.2f} s)",
                 "per_process_accesses_per_s": [r[1] / r[2] for r in res]}
@@ -552,7 +583,7 @@ def single_instance(cfg, args, dev, threads, replay: int = 0) -> dict:
     return {"value": done / (ms / 1e3), "unit": "accesses/s", "requests": int(done), "kernel_ms": ms, "wall_s": wall,
             "mg1_share_of_link_visits": (st["mg1_calls"] - before["mg1_calls"]) /
                                         max(1, st["net_distance"] - before["net_distance"]),
-            "sample": f"one C4 simulation alone on the GPU (replica 0's stream, {mode}): {n_w} warmup requests, then "
+            "sample": f"one {WORKLOAD} simulation alone on the GPU (replica 0's stream, {mode}): {n_w} warmup requests, then "
                       f"{n_t} requests in one launch; link visits/access "
                       f"{(st['net_distance'] - before['net_distance']) / max(1, done):.1f}",
             "note": "one uncore is a sequential fold (one wavefront); DESIGN.md §1a measures how little of it a "
@@ -632,12 +663,19 @@ def parse_args(argv=None):
     ap.add_argument("--single-requests", type=int, default=40960)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="headline only (profiling runs)")
-    ap.add_argument("--replay", choices=("open", "closed"), default="open",
-                    help="headline replay mode (open: the metric; closed: profiling / A/B runs of the realistic regime)")
+    ap.add_argument("--config", choices=sorted(WORKLOADS), default="C4",
+                    help="SURVEY.md §8d shape: C4 (1024 cores) is the metric's; C3 (256 cores, 3 levels) and C5 "
+                         "(4096 cores) are measured the same way")
+    ap.add_argument("--replay", choices=("open", "closed"), default=None,
+                    help="headline replay mode (open: the metric; closed: profiling / A/B runs of the realistic "
+                         "regime); default: the configuration's (open for C3/C4, closed for C5)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) normally; gloo for CPU-side rehearsal")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC traffic summary written by tools/pmc_traffic.py for this build")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if a.replay is None:
+        a.replay = WORKLOADS[a.config]["replay"]
+    return a
 
 
 class Device:
@@ -712,7 +750,9 @@ def main(argv=None) -> None:
     from primesim_amd import config as CF
     from primesim_amd.dist import gather_objects, reduce_run, replica_seed
 
-    sim = CF.preset("C4")
+    global WORKLOAD
+    WORKLOAD = args.config
+    sim = CF.preset(WORKLOAD)
     xml_path = os.path.join(tempfile.gettempdir(), f"pu_bench_c4_{os.getpid()}.xml")
     CF.write_xml(sim, xml_path)
     cfg = P.load_config(xml_path)
@@ -726,7 +766,8 @@ def main(argv=None) -> None:
     rank_parity = world > 1 and not args.no_cpu and args.rank_parity_workers > 0
     if (extras and not args.no_cpu) or rank_parity:
         nw = (args.ensemble_workers or host_core_share()) if extras else args.rank_parity_workers
-        ens = Ensemble(xml_path, nw, args.warmup * args.chunk, args.steps * args.chunk, args.ensemble_seconds, rank)
+        ens = Ensemble(xml_path, nw, args.warmup * args.chunk, args.steps * args.chunk, args.ensemble_seconds, rank,
+                       ref_mode(args))
 
     import torch.distributed as dist
     if world > 1:
@@ -790,7 +831,7 @@ def main(argv=None) -> None:
     if rank == 0:
         replica_parity_res = rparity if world == 1 else None
         closed = None
-        if extras and args.closed_steps > 0:
+        if extras and args.closed_steps > 0 and args.replay == "open":
             um.reset()
             C = run_pass(um, args, R, rank, world, dev, stream, P.uncore.PU_REPLAY_CLOSED, args.closed_steps,
                          [0], D.slots)
@@ -805,7 +846,7 @@ def main(argv=None) -> None:
                 c_par = {"kind": kind, "requests_compared": m, "bit_identical": bool(np.array_equal(gd[:m], d_cpu[:m]))}
                 parity_ok &= c_par["bit_identical"]
                 c_cpu = {"value": n_cpu / el, "unit": "accesses/s", "cores": 1, "kind": kind, "cpu_model": cpu_model(),
-                         "sample": f"replica 0's C4 stream replayed closed-loop: requests {w0}..{w0 + n_cpu} after an "
+                         "sample": f"replica 0's {WORKLOAD} stream replayed closed-loop: requests {w0}..{w0 + n_cpu} after an "
                                    f"untimed closed-loop fill of {w0}, single-threaded "
                                    f"({'reference uncore compiled from /root/reference/src, no counting wraps' if kind == 'reference' else 'oracle/cpu_ref restatement'}), "
                                    f"{el:.1f} s"}
@@ -825,7 +866,8 @@ def main(argv=None) -> None:
             log(f"[bench] closed loop: {closed['value']:.4g} accesses/s, halted {C.halted}, "
                 f"M/G/1 share {closed['mg1_share_of_link_visits']:.3f}")
         um.close()
-        single = single_instance(cfg, args, dev, threads) if extras else None
+        single = single_instance(cfg, args, dev, threads,
+                                 P.uncore.PU_REPLAY_CLOSED if args.replay == "closed" else 0) if extras else None
         if single:
             log(f"[bench] single instance: {single['value']:.0f} accesses/s")
         if closed is not None:
@@ -838,13 +880,13 @@ def main(argv=None) -> None:
             # --cpu-seconds); parity is checked on every request both ran
             w0, n_t = args.warmup * args.chunk, args.steps * args.chunk
             s0 = P.generate_stream(stream_spec(replica_seed(SEED_BASE, rank, 0), w0 + n_t))
-            kind, n_cpu, el, d_cpu = cpu_baseline(xml_path, cfg, s0, threads, w0, args.cpu_seconds)
+            kind, n_cpu, el, d_cpu = cpu_baseline(xml_path, cfg, s0, threads, w0, args.cpu_seconds, ref_mode(args))
             gpu_d = H.kept[0]
             m = min(len(d_cpu), len(gpu_d))
             parity = bool(np.array_equal(gpu_d[:m], d_cpu[:m]))
             parity_ok &= parity
             cpu = {"value": n_cpu / el, "unit": "accesses/s", "cores": 1, "kind": kind, "cpu_model": cpu_model(),
-                   "sample": f"replica 0's C4 stream: requests {w0}..{w0 + n_cpu} (the GPU's timed window; the GPU "
+                   "sample": f"replica 0's {WORKLOAD} stream ({args.replay} loop): requests {w0}..{w0 + n_cpu} (the GPU's timed window; the GPU "
                              f"ran {int(H.adv[0])} of them for replica 0), after an untimed fill of the {w0}-request "
                              f"warmup, single-threaded "
                              f"({'reference uncore compiled from /root/reference/src, no counting wraps' if kind == 'reference' else 'oracle/cpu_ref restatement'}), "
@@ -872,7 +914,8 @@ def main(argv=None) -> None:
                 traffic_src = (f"not reported: {os.path.relpath(args.traffic_json, ROOT)} was measured on build "
                                f"{tj.get('src_hash')}, this library is {built}")
         result = {
-            "metric": METRIC,
+            "metric": METRIC if WORKLOAD == "C4" else
+                      METRIC.replace("at 1024 cores", f"at {WORKLOADS[WORKLOAD]['cores']} cores ({WORKLOAD})"),
             "value": value,
             "unit": "accesses/s",
             "n_gpus": world,
@@ -885,8 +928,7 @@ def main(argv=None) -> None:
             "dtype": "int64",
             "data": "synthetic",
             "config": {
-                "workload": "C4: 1024-core 32x32 mesh, L1 32KB/8W + 256KB/8W shared-LLC slice per tile, "
-                            "directory MESI full-map, uniform 2^20 lines + 64-line hotspot, 25% writes, open-loop replay",
+                "workload": f"{WORKLOADS[WORKLOAD]['desc']}, {args.replay}-loop replay",
                 "replicas_per_gpu": R,
                 "replicas_total": tot_replicas,
                 "wavefronts_per_gpu": D.slots,

@@ -11,6 +11,7 @@
 #   traffic      PMC fabric traffic of the headline kernel on the driver's window (tools/pmc_traffic.py)
 #   bench        bench.py on the driver's config (--steps 20 --warmup 5), carrying TAG_traffic.json if present
 #   bench_default  bench.py with no flags
+#   bench_c3 / bench_c5  bench.py --config C3 / C5 on the driver's window (C5 closed loop by default)
 #   rocprof      rocprofv3 --kernel-trace --stats of the driver's config (headline only)
 #   sq           SQ wave-state / instruction counters of the headline kernel (tools/pmc_sq.py)
 #   sq_single    the same for one simulation alone, open loop and closed loop (latency kernel)
@@ -75,6 +76,8 @@ for S in "$@"; do
     traffic) timeout -k 10 500 python tools/pmc_traffic.py --work /tmp/pmc --out ${O}_traffic.json -- $DRIVER --no-cpu --no-extras > ${O}_traffic.log 2>&1 || exit 1;;
     bench) TJ=""; [ -f ${O}_traffic.json ] && TJ="--traffic-json ${O}_traffic.json"
            timeout -k 10 400 $BENCH $DRIVER $TJ > ${O}_bench.json 2> ${O}_bench.log || exit 1;;
+    bench_c3) timeout -k 10 500 $BENCH --config C3 $DRIVER > ${O}_bench_c3.json 2> ${O}_bench_c3.log || exit 1;;
+    bench_c5) timeout -k 10 600 $BENCH --config C5 $DRIVER > ${O}_bench_c5.json 2> ${O}_bench_c5.log || exit 1;;
     bench_default) timeout -k 10 400 $BENCH > ${O}_bench_default.json 2> ${O}_bench_default.log || exit 1;;
     rocprof) TJ=""; [ -f ${O}_traffic.json ] && TJ="--traffic-json ${O}_traffic.json"
              timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/${T}_prof -o run -- python3 bench.py $DRIVER --no-cpu --no-extras $TJ > ${O}_bench_under_rocprof.json 2> ${O}_rocprof.log || exit 1
