@@ -362,6 +362,25 @@ int pu_access_status(pu_handle* h, int core_id, int prog_id, int mem_type,
 int pu_access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n,
                     int32_t* delay_out);
 
+/* Resident mode (no reference counterpart; the transport under prime.cpp:129's
+ * per-request uncore_access and the per-message batch): pu_access,
+ * pu_access_status and pu_access_batch of at most 16,384 requests do not
+ * launch a kernel per call.  The first such call starts one persistent
+ * latency-mode workgroup for that replica, which keeps the replica's queue
+ * headers in its CU's LDS and takes every later call through a mailbox in
+ * host-coherent pinned memory (requests in, delays and error flags out), each
+ * call computing exactly what one launch would.  It leaves by itself after
+ * PRIMEUNCORE_RESIDENT_IDLE_MS (default 50) without a call, when another
+ * replica or a launch of any kind needs the engine, on pu_reset, pu_synchronize,
+ * a read of statistics, completion cycles or the report, and on pu_destroy or
+ * process exit.  It needs the compiled configuration and a replica whose queue
+ * headers fit one CU's LDS; otherwise (or with PRIMEUNCORE_RESIDENT=0) every
+ * call launches as before.  pu_set_resident: mode 1 on, 0 off (joins a running
+ * kernel), -1 query; returns the previous mode.  pu_resident_info writes
+ * {kernel running, commands served, kernels launched, eligible}. */
+int pu_set_resident(pu_handle* h, int mode);
+int pu_resident_info(pu_handle* h, uint64_t* out4);
+
 /* Batch path from device memory, all replicas at once, asynchronous on
  * `hip_stream` (a hipStream_t; NULL = the engine's own stream, see
  * pu_synchronize).  Replica r
@@ -417,7 +436,8 @@ int pu_stats_get(pu_handle* h, int replica, pu_stats* out);
 long pu_report(pu_handle* h, int replica, int include_time, char* buf, size_t cap);
 
 /* Device-time of the last pu_run_device / pu_access_batch launch, in ms,
- * measured with HIP events on the engine's stream. */
+ * measured with HIP events on the engine's stream (a call served by the
+ * resident kernel: its wall time from posting to the answer). */
 double pu_last_kernel_ms(pu_handle* h);
 
 /* UncoreManager::getSimStartTime / getSimFinishTime (uncore_manager.cpp:52-60):

@@ -2709,6 +2709,129 @@ __device__ __forceinline__ bool replica_run(Engine<NL, LH>& e, char* __restrict_
     return done;
 }
 
+
+// Resident mode (MODE 3, latency kernels only; geometry.h PuMailbox): one
+// two-wave workgroup stays on the GPU for replica `rep` and serves the host's
+// commands — a lone uncore_access (uncore_manager.cpp:82-85, prime.cpp:129)
+// or a short host batch — without a launch per call, with the replica's
+// queue headers kept in the CU's LDS image across calls (the ~17 µs image copy
+// of a latency launch is paid once).  Each command is exactly one launch's
+// work: replica_loop over the requests (copied from the host's mailbox into
+// device memory first) and replica_close (run state and counters back to
+// HBM), so results are those of the launch path.  Delays go straight into the
+// host buffer; `ack` is published after a system-scope release, so the host
+// sees every delay, every counter and the run state when it sees the ack.
+// The kernel leaves on a STOP command or after `idle_ticks` (s_memrealtime,
+// 100 MHz) without one: a persistent kernel that always drains by itself.
+struct ResCtl {
+    uint64_t seq;      // the last command taken
+    uint64_t n;        // its requests
+    uint64_t err;      // the replica's error flags (EngineStats.error_flags)
+    uint32_t flags, cmd;
+};
+static __shared__ ResCtl lds_res;
+
+// (relaxed: a system-scope load reads the host's value without invalidating
+// the caches at every poll; the acquire fence follows once the value changed)
+__device__ __forceinline__ uint64_t sys_load_u64(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <int NL>
+__device__ __forceinline__ void resident_body(const Geo* __restrict__ g, char* __restrict__ arena, int rep,
+                                              pu_req* __restrict__ stage, PuMailbox* mb, uint64_t idle_ticks,
+                                              uint64_t cap) {
+    constexpr bool LH = true;                 // (OFF)
+    Engine<NL, LH> e;
+    e.g = g;
+    e.ln = lane_id();
+    const bool helper = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 64;
+    e.base = arena + (size_t)rep * OFF(g->replica_bytes);
+    char* hb = e.base + OFF(g->off_qhdr);
+    const uint32_t nq = (uint32_t)g->nqueues;
+    const AS1 v4u32* hreq = (const AS1 v4u32*)(AS1 char*)(char*)(mb + 1);
+    int32_t* hdelay = reinterpret_cast<int32_t*>(reinterpret_cast<pu_req*>(mb + 1) + cap);
+    hdr_image_in(hb, nq, threadIdx.x);        // threads 0..127: pieces t, t + 128, ...
+    if (!helper && e.ln == 0) {
+        lds_res.seq = sys_load_u64(&mb->d.ack);   // the host sets ack = seq before the launch
+        lds_res.err = e.template at<EngineStats>(OFF(g->off_stats))->error_flags;
+    }
+    __syncthreads();
+    for (;;) {
+        if (!helper) {
+            // lane 0 polls the host's command word; the other lanes wait with it
+            const uint64_t last = uni64(lds_res.seq);
+            const uint64_t t_idle = __builtin_amdgcn_s_memrealtime() + idle_ticks;
+            uint64_t sq = last;
+            for (;;) {
+                if (e.ln == 0) sq = sys_load_u64(&mb->h.seq);
+                sq = rl64(sq, 0);
+                if (sq != last || __builtin_amdgcn_s_memrealtime() >= t_idle) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (sq != last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // the command's fields and requests
+            if (e.ln == 0) {
+                if (sq != last) {
+                    const volatile PuResHost* H = &mb->h;
+                    lds_res.n = H->n;
+                    lds_res.flags = H->flags;
+                    lds_res.cmd = H->cmd;
+                    lds_res.seq = sq;
+                } else {
+                    lds_res.cmd = PU_RES_STOP;        // idle: leave
+                }
+            }
+        }
+        __syncthreads();                              // [A] the command is in LDS
+        if (uni32(lds_res.cmd) != PU_RES_RUN) break;
+        const uint64_t n = min(uni64(lds_res.n), cap);
+        if (helper) {
+            __syncthreads();                          // [B] replica_loop's stats_init
+            mg1_helper(g, e.base, stage, 0, n);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no prefetch DMA outlives the command
+            __syncthreads();                          // [C] the main wave left its loop
+            __syncthreads();                          // [D] replica_close
+            continue;
+        }
+        {   // the requests: host mailbox -> device staging, 16 B per lane and step, 4 steps in flight
+            AS1 v4u32* dst = (AS1 v4u32*)(AS1 char*)(char*)stage;
+            const uint64_t pieces = 2 * n;
+            for (uint64_t k = (uint64_t)e.ln; k < pieces; k += 256) {
+                v4u32 a0 = v4u32{0u, 0u, 0u, 0u}, a1 = a0, a2 = a0, a3 = a0;
+                a0 = hreq[k];
+                if (k + 64 < pieces) a1 = hreq[k + 64];
+                if (k + 128 < pieces) a2 = hreq[k + 128];
+                if (k + 192 < pieces) a3 = hreq[k + 192];
+                dst[k] = a0;
+                if (k + 64 < pieces) dst[k + 64] = a1;
+                if (k + 128 < pieces) dst[k + 128] = a2;
+                if (k + 192 < pieces) dst[k + 192] = a3;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (e.ln == 0) {
+            lds_hq_head = 0;
+            lds_main_done = 0;
+        }
+        replica_loop<NL, false, LH>(e, stage, hdelay, 0, n, nullptr, UINT64_MAX, uni32(lds_res.flags));   // [B]
+        if (e.ln == 0) *(volatile AS3 uint32_t*)&lds_main_done = 1u;
+        __syncthreads();                              // [C]
+        replica_close<NL, LH>(e);                     // [D]
+        if (e.ln == 0) {
+            lds_res.err |= lds_err;
+            volatile PuResDev* Dv = &mb->d;
+            Dv->err = lds_res.err;
+            Dv->last_addr = lds_eng.last_addr;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: delays, counters, run state visible
+        if (e.ln == 0) __hip_atomic_store(&mb->d.ack, uni64(lds_res.seq), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    hdr_image_out(hb, nq, threadIdx.x);              // the headers back to HBM
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (!helper && e.ln == 0) __hip_atomic_store(&mb->d.exited, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // One workgroup (= one wavefront) per replica.  Replica replica0 + blockIdx.x
 // processes reqs[off[blockIdx.x] .. off[blockIdx.x+1]) in order (replica_loop).
 //
@@ -2729,7 +2852,9 @@ __device__ __forceinline__ bool replica_run(Engine<NL, LH>& e, char* __restrict_
 // the same slice, so no wave idles while replicas remain.  nrep = replicas.
 // Each slot adds its wave's lifetime in s_memrealtime ticks to a counter
 // (the host's busy-time accounting).
-// MODE: 0 fixed ranges, 1 time-sliced, 2 replica pool (time-sliced); each a
+// MODE: 0 fixed ranges, 1 time-sliced, 2 replica pool (time-sliced), 3
+// resident (latency kernels: reqs = device staging, off = the host mailbox,
+// budget_ticks = idle ticks, nrep = staging capacity; resident_body); each a
 // separate instantiation, so the pool's bookkeeping costs the others nothing
 // and profiles list the launch kinds apart.
 template <int NL, int MODE, bool LH>
@@ -2738,6 +2863,12 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
                                             int32_t* __restrict__ delays, uint64_t* __restrict__ pos,
                                             uint64_t budget_ticks, uint32_t flags, uint32_t* __restrict__ sched,
                                             int nrep) {
+  if constexpr (MODE == 3) {
+    static_assert(LH, "resident mode runs the latency kernel");
+    resident_body<NL>(g, arena, replica0, const_cast<pu_req*>(reqs),
+                      reinterpret_cast<PuMailbox*>(const_cast<uint64_t*>(off)), budget_ticks, (uint64_t)nrep);
+    (void)delays; (void)pos; (void)flags; (void)sched;
+  } else {
     constexpr bool SLICED = MODE >= 1;
     constexpr bool pool = MODE == 2 && !LH;
     if constexpr (!SLICED) {
@@ -2795,6 +2926,7 @@ __device__ __forceinline__ void uncore_body(const Geo* __restrict__ g, char* __r
                 __builtin_amdgcn_s_memrealtime() - wave_t0;
         }
     }
+  }
 }
 
 #ifndef PU_JIT_GEO
@@ -2829,6 +2961,7 @@ PU_JIT_KERNEL(pu_jit_uncore_s2_h0, 2, false)
 #if !defined(PU_JIT_PART) || PU_JIT_PART == 1
 PU_JIT_KERNEL(pu_jit_uncore_s0_h1, 0, true)
 PU_JIT_KERNEL(pu_jit_uncore_s1_h1, 1, true)
+PU_JIT_KERNEL(pu_jit_uncore_s3_h1, 3, true)
 #endif
 namespace {
 #endif

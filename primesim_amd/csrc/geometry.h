@@ -207,6 +207,38 @@ struct Geo {
 #define PU_KF_REQ16    8u   // d_reqs holds 16-B pu_req16 records (pu_set_device_req_format;
                             // throughput launches only)
 
+// Resident mode (pu_access / short host batches without a launch per call):
+// one latency-mode workgroup stays on the GPU with the replica's queue
+// headers in its CU's LDS and serves commands through a mailbox in
+// host-coherent pinned memory.  The host writes the requests, then the
+// command, then `seq`; the kernel (lane 0 polling `seq` with system-scope
+// acquire loads) copies the requests into device memory, runs them exactly as
+// one launch would (replica_loop + replica_close), writes every delay into the
+// host buffer, then error flags and last_addr, and publishes `ack = seq` after
+// a system-scope release.  It leaves (headers back to HBM, `exited = 1`) on a
+// STOP command or after `idle` ticks without one.
+#define PU_RES_RUN 0u
+#define PU_RES_STOP 1u
+struct PuResHost {          // written by the host (its own 64-B line)
+    uint64_t seq;           // command number: the kernel waits for a change
+    uint64_t n;             // requests of the command (in PuMailbox's request area)
+    uint32_t flags;         // PU_KF_* of the command
+    uint32_t cmd;           // PU_RES_RUN / PU_RES_STOP
+    uint64_t _pad[5];
+};
+struct PuResDev {           // written by the kernel (its own 64-B line)
+    uint64_t ack;           // seq of the last command completed
+    uint64_t err;           // the replica's EngineStats.error_flags after it
+    uint64_t last_addr;     // RunState.last_addr after it (TLB translation)
+    uint32_t exited, _pad0; // 1 once the kernel has left (stop or idle)
+    uint64_t _pad[4];
+};
+// Mailbox: {host line, device line}, then pu_req reqs[cap], then int32 delays[cap].
+struct PuMailbox {
+    PuResHost h;
+    PuResDev d;
+};
+
 // Per-replica run state carried across launches.
 struct RunState {
     int32_t batch_delay;   // prime.cpp:113 running `delay` of the open message

@@ -236,8 +236,8 @@ bool offline_allowed() {
 }
 
 // The offline compiler's identity for the cache key: the resolved driver and
-// clang paths with their size and modification time, and the ROCm version
-// file — no child process (jit_key also runs in processes that use the GPU).
+// clang paths with their sizes, and the ROCm version file — no child process
+// (jit_key also runs in processes that use the GPU).
 const std::string& offline_cc_identity() {
     static const std::string id = [] {
         std::string s;
@@ -248,8 +248,8 @@ const std::string& offline_cc_identity() {
                 s += "|-";
                 return;
             }
-            s += std::string("|") + rp + ":" + std::to_string((long long)st.st_size) + ":" +
-                 std::to_string((long long)st.st_mtime);
+            // (no modification time: the GPU boxes unpack the same image with their own times)
+            s += std::string("|") + rp + ":" + std::to_string((long long)st.st_size);
         };
         const std::string cc = offline_cc();
         add(cc);
@@ -406,10 +406,11 @@ bool load_module(const std::vector<char>& code, int part, JitKernels* out, std::
         *why = "the device refused the code object";
         return false;
     }
-    static const char* names[3][2] = {{"pu_jit_uncore_s0_h0", "pu_jit_uncore_s0_h1"},
+    static const char* names[4][2] = {{"pu_jit_uncore_s0_h0", "pu_jit_uncore_s0_h1"},
                                       {"pu_jit_uncore_s1_h0", "pu_jit_uncore_s1_h1"},
-                                      {"pu_jit_uncore_s2_h0", nullptr}};
-    for (int s = 0; s < 3; s++)
+                                      {"pu_jit_uncore_s2_h0", nullptr},
+                                      {nullptr, "pu_jit_uncore_s3_h1"}};
+    for (int s = 0; s < 4; s++)
         if (names[s][part] && hipModuleGetFunction(&out->f[s][part], mod, names[s][part]) != hipSuccess) {
             (void)hipModuleUnload(mod);
             *why = std::string("the code object lacks ") + names[s][part];
@@ -585,6 +586,21 @@ int jit_launch(const JitKernels& k, bool sliced, bool lds_headers, int nblocks, 
     hipFunction_t f = sched ? k.f[2][0] : k.f[sliced ? 1 : 0][lds_headers ? 1 : 0];
     hipError_t e = hipModuleLaunchKernel(f, (unsigned)nblocks, 1, 1,
                                          lds_headers ? 128 : 64, 1, 1, 0, stream, args, nullptr);
+    return e == hipSuccess ? 0 : PU_EIO;
+}
+
+int jit_launch_resident(const JitKernels& k, hipStream_t stream, const Geo* d_geo, char* arena, int replica,
+                        pu_req* stage, void* mbox, uint64_t idle_ticks, int cap) {
+    if (!k.f[3][1]) return PU_EINVAL;
+    const pu_req* reqs = stage;
+    const uint64_t* off = reinterpret_cast<const uint64_t*>(mbox);
+    int32_t* delays = nullptr;
+    uint64_t* pos = nullptr;
+    uint32_t flags = 0;
+    uint32_t* sched = nullptr;
+    void* args[] = {(void*)&d_geo, (void*)&arena, (void*)&replica, (void*)&reqs, (void*)&off,
+                    (void*)&delays, (void*)&pos, (void*)&idle_ticks, (void*)&flags, (void*)&sched, (void*)&cap};
+    hipError_t e = hipModuleLaunchKernel(k.f[3][1], 1, 1, 1, 128, 1, 1, 0, stream, args, nullptr);
     return e == hipSuccess ? 0 : PU_EIO;
 }
 

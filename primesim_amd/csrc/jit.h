@@ -11,8 +11,9 @@
 namespace pu {
 
 // The launch shapes of the engine compiled for one configuration: fixed
-// ranges / time-sliced / replica pool (f[0..2]) x queue headers in HBM or in
-// LDS (f[.][0..1]; the pool runs with headers in HBM only).
+// ranges / time-sliced / replica pool / resident (f[0..3]) x queue headers in
+// HBM or in LDS (f[.][0..1]; the pool runs with headers in HBM only, the
+// resident kernel with headers in LDS only).
 // Code objects come from the offline compiler (hipcc, at build time: jit_warm)
 // or from hipRTC (in-process, on a cache miss at run time).
 constexpr int kJitRtc = 0, kJitOffline = 1;
@@ -22,7 +23,7 @@ constexpr int kJitParts = 2;
 struct JitKernels {
     hipModule_t mod[kJitParts] = {nullptr, nullptr};
     int cc[kJitParts] = {0, 0};   // kJitRtc / kJitOffline: which compiler built each part
-    hipFunction_t f[3][2] = {{nullptr, nullptr}, {nullptr, nullptr}, {nullptr, nullptr}};
+    hipFunction_t f[4][2] = {{nullptr, nullptr}, {nullptr, nullptr}, {nullptr, nullptr}, {nullptr, nullptr}};
     bool ok = false;
     std::string key;
 };
@@ -42,6 +43,12 @@ int jit_prof_read(unsigned long long* out, int n, int reset);
 int jit_launch(const JitKernels& k, bool sliced, bool lds_headers, int nblocks, hipStream_t stream, const Geo* d_geo,
                char* arena, int replica0, const pu_req* reqs, const uint64_t* off, int32_t* delays, uint64_t* pos,
                uint64_t budget_ticks, uint32_t flags, uint32_t* sched = nullptr, int nrep = 0);
+// The resident kernel (engine.hip resident_body) for replica `replica`: one
+// two-wave workgroup on `stream` serving the mailbox `mbox` (device-visible
+// pointer) with `stage` (cap requests of device memory) until a STOP command
+// or `idle_ticks` of s_memrealtime without one.
+int jit_launch_resident(const JitKernels& k, hipStream_t stream, const Geo* d_geo, char* arena, int replica,
+                        pu_req* stage, void* mbox, uint64_t idle_ticks, int cap);
 // One-wave workgroups of the throughput kernel of launch mode `mode` (1
 // time-sliced, 2 replica pool) per CU by hipOccupancy, and its static LDS bytes.
 int jit_occupancy(const JitKernels& k, int mode, int* blocks_per_cu, int* lds_bytes);

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <ctime>
@@ -313,6 +314,23 @@ struct pu_handle {
     int32_t* h_delays = nullptr; // pinned: delays[cap]
     uint64_t* h_tail = nullptr;  // pinned: error flags, RunState
     size_t stage_cap = 0;
+    // Resident mode (engine.hip resident_body; geometry.h PuMailbox): one
+    // latency-mode workgroup serving pu_access / short host batches of one
+    // replica through a mailbox in host-coherent pinned memory
+    struct Resident {
+        int mode = 1;               // PRIMEUNCORE_RESIDENT (0 off) / pu_set_resident
+        bool running = false;       // a resident kernel was launched and not yet joined
+        int replica = -1;
+        uint64_t seq = 0;           // commands posted
+        uint64_t acked = 0;         // commands completed
+        PuMailbox* mb = nullptr;    // host address
+        void* mb_dev = nullptr;     // the same memory, as the device sees it
+        pu_req* stage = nullptr;    // device staging of a command's requests
+        hipStream_t stream = nullptr;
+        hipEvent_t after = nullptr; // orders the kernel after the handle's stream
+        uint64_t idle_ticks = 5000000;   // 50 ms of s_memrealtime (100 MHz)
+        uint64_t commands = 0, launches = 0;
+    } res;
     std::mutex mu;
 };
 
@@ -351,6 +369,9 @@ constexpr size_t kOffBytes = 64;   // offsets, padded so the requests start on a
 constexpr size_t kTailBytes = 8 + sizeof(RunState);
 constexpr size_t kShortBatch = 16384;   // host batches below this skip the LDS header image
 
+int resident_stop(pu_handle* h);
+void resident_free(pu_handle* h);
+
 void free_stage(pu_handle* h) {
     if (h->d_off) (void)hipFree(h->d_off);   // d_reqs lives in the same block
     if (h->d_delays) (void)hipFree(h->d_delays);
@@ -369,6 +390,8 @@ void free_stage(pu_handle* h) {
 int ensure_stage(pu_handle* h, size_t n) {
     if (n <= h->stage_cap && h->d_off) return 0;
     size_t cap = n < 4096 ? 4096 : n;
+    int rc = resident_stop(h);   // hipFree may wait for the whole device
+    if (rc) return rc;
     free_stage(h);
     const size_t in_bytes = kOffBytes + cap * sizeof(pu_req);
     void* p = nullptr;
@@ -399,9 +422,158 @@ int wait_stream(hipStream_t s) {
     return 0;
 }
 
+// ---- resident mode (the caller holds h->mu) ----
+constexpr size_t kResCap = 16384;   // requests per command (= the short-batch bound)
+
+size_t res_bytes() { return sizeof(PuMailbox) + kResCap * (sizeof(pu_req) + sizeof(int32_t)); }
+
+// Join the resident kernel: a STOP command unless it already left (idle), then
+// wait for its stream.  Its headers are back in HBM afterwards.
+int resident_stop(pu_handle* h) {
+    auto& R = h->res;
+    if (!R.running) return 0;
+    volatile PuMailbox* mb = R.mb;
+    if (!mb->d.exited) {
+        mb->h.cmd = PU_RES_STOP;
+        mb->h.n = 0;
+        std::atomic_thread_fence(std::memory_order_release);
+        mb->h.seq = ++R.seq;
+    }
+    R.running = false;
+    HIP_TRY(hipStreamSynchronize(R.stream), PU_EIO);
+    R.acked = mb->d.ack;
+    R.seq = R.acked;   // a STOP is never acked; the next kernel starts from the last completed command
+    return 0;
+}
+
+// Every handle with a resident kernel, joined at process exit through the
+// mailbox alone (the kernel leaves by itself within the idle time anyway).
+std::mutex g_res_mu;
+std::vector<pu_handle*> g_res_handles;
+void resident_atexit() {
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    for (pu_handle* h : g_res_handles) {
+        auto& R = h->res;
+        if (!R.running || !R.mb) continue;
+        volatile PuMailbox* mb = R.mb;
+        mb->h.cmd = PU_RES_STOP;
+        std::atomic_thread_fence(std::memory_order_release);
+        mb->h.seq = ++R.seq;
+        const auto t0 = std::chrono::steady_clock::now();
+        while (!mb->d.exited && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2)) {}
+    }
+}
+
+bool resident_eligible(const pu_handle* h, size_t n) {
+    return h->res.mode && h->jit.ok && h->jit.f[3][1] && h->lds_headers_ok && n <= kResCap;
+}
+
+// A resident kernel for `replica` is running (started or restarted here).
+int resident_ensure(pu_handle* h, int replica) {
+    auto& R = h->res;
+    if (R.running && R.replica == replica && !((volatile PuMailbox*)R.mb)->d.exited) return 0;
+    int rc = resident_stop(h);
+    if (rc) return rc;
+    if (!R.mb) {
+        void* p = nullptr;
+        HIP_TRY(hipHostMalloc(&p, res_bytes(), hipHostMallocCoherent | hipHostMallocMapped), PU_ENOMEM);
+        std::memset(p, 0, res_bytes());
+        R.mb = (PuMailbox*)p;
+        HIP_TRY(hipHostGetDevicePointer(&R.mb_dev, p, 0), PU_EIO);
+        HIP_TRY(hipMalloc(&R.stage, kResCap * sizeof(pu_req)), PU_ENOMEM);
+        HIP_TRY(hipStreamCreateWithFlags(&R.stream, hipStreamNonBlocking), PU_EIO);
+        HIP_TRY(hipEventCreateWithFlags(&R.after, hipEventDisableTiming), PU_EIO);
+        std::lock_guard<std::mutex> lk(g_res_mu);
+        if (g_res_handles.empty()) std::atexit(resident_atexit);
+        g_res_handles.push_back(h);
+    }
+    volatile PuMailbox* mb = R.mb;
+    mb->d.exited = 0;
+    mb->d.ack = R.acked;   // the kernel waits for seq != ack: a posted, unacked command runs first
+    mb->h.seq = R.seq;
+    std::atomic_thread_fence(std::memory_order_release);
+    // after everything already queued on the handle's stream (the header image it copies in)
+    HIP_TRY(hipEventRecord(R.after, h->stream), PU_EIO);
+    HIP_TRY(hipStreamWaitEvent(R.stream, R.after, 0), PU_EIO);
+    if (pu::jit_launch_resident(h->jit, R.stream, h->d_geo, h->arena, replica, R.stage, R.mb_dev, R.idle_ticks,
+                                (int)kResCap) != 0)
+        return pu::set_error(PU_EIO, "resident kernel launch failed");
+    R.running = true;
+    R.replica = replica;
+    R.launches++;
+    return 0;
+}
+
+// One command: the requests through the resident kernel; delays, error flags
+// and (TLB) the last translated address come back through the mailbox.
+int resident_run(pu_handle* h, int replica, const pu_req* reqs, size_t n, uint32_t flags, int32_t* delay_out,
+                 uint64_t* err_out, uint64_t* last_addr) {
+    auto& R = h->res;
+    int rc = resident_ensure(h, replica);
+    if (rc) return rc;
+    volatile PuMailbox* mb = R.mb;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::memcpy(R.mb + 1, reqs, n * sizeof(pu_req));
+    mb->h.n = n;
+    mb->h.flags = flags;
+    mb->h.cmd = PU_RES_RUN;
+    std::atomic_thread_fence(std::memory_order_release);
+    const uint64_t seq = ++R.seq;
+    mb->h.seq = seq;
+    for (uint64_t spin = 1;; spin++) {
+        if (mb->d.ack == seq) break;
+        if ((spin & 1023) == 0) {
+            if (mb->d.exited && mb->d.ack != seq) {
+                // it left (idle) just before the command arrived: a new kernel takes it
+                R.running = false;
+                HIP_TRY(hipStreamSynchronize(R.stream), PU_EIO);
+                R.acked = mb->d.ack;
+                rc = resident_ensure(h, replica);
+                if (rc) return rc;
+                continue;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+                R.mode = 0;   // never again on this handle
+                return pu::set_error(PU_EIO, "resident kernel did not answer within 60 s");
+            }
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    R.acked = seq;
+    R.commands++;
+    if (delay_out) std::memcpy(delay_out, (const int32_t*)((const pu_req*)(R.mb + 1) + kResCap), n * sizeof(int32_t));
+    *err_out = mb->d.err;
+    if (last_addr) *last_addr = mb->d.last_addr;
+    h->last_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+}
+
+void resident_free(pu_handle* h) {
+    auto& R = h->res;
+    (void)resident_stop(h);
+    {
+        std::lock_guard<std::mutex> lk(g_res_mu);
+        for (size_t i = 0; i < g_res_handles.size(); i++)
+            if (g_res_handles[i] == h) {
+                g_res_handles.erase(g_res_handles.begin() + (long)i);
+                break;
+            }
+    }
+    if (R.stage) (void)hipFree(R.stage);
+    if (R.mb) (void)hipHostFree(R.mb);
+    if (R.after) (void)hipEventDestroy(R.after);
+    if (R.stream) (void)hipStreamDestroy(R.stream);
+    R.stage = nullptr;
+    R.mb = nullptr;
+    R.after = nullptr;
+    R.stream = nullptr;
+}
+
 int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const uint64_t* d_off, int32_t* d_delay,
            hipStream_t s, uint64_t* d_pos = nullptr, uint64_t budget_ticks = 0, uint32_t extra_flags = 0,
            bool short_launch = false, bool use_replay_mode = true, uint32_t* d_sched = nullptr) {
+    int rrc = resident_stop(h);   // a launch reads the queue headers from HBM
+    if (rrc) return rrc;
     HIP_TRY(hipEventRecord(h->ev0, s), PU_EIO);
     // latency mode: with at most one replica per CU each wave keeps its queue
     // headers in the CU's LDS for the launch (engine.hip, LH). Copying the
@@ -431,6 +603,8 @@ int launch(pu_handle* h, int replica0, int nblocks, const pu_req* d_reqs, const 
 // Gathers EngineStats.error_flags of replicas [0, n) (one strided copy).
 int gather_error_flags(pu_handle* h, uint64_t* out, size_t n) {
     if (n == 0) return 0;
+    int rrc = resident_stop(h);
+    if (rrc) return rrc;
     const Geo& g = h->geo;
     HIP_TRY(hipStreamSynchronize(h->stream), PU_EIO);
     HIP_TRY(hipMemcpy2D(out, sizeof(uint64_t), h->arena + g.off_stats + offsetof(EngineStats, error_flags),
@@ -454,8 +628,15 @@ int limit_error(uint64_t flags, int replica) {
 }
 
 // Copies replica r's engine-side counters.
+int resident_quiesce(pu_handle* h) {   // (unlocked callers) the engine state in HBM is current
+    std::lock_guard<std::mutex> lk(h->mu);
+    return resident_stop(h);
+}
+
 int read_replica(pu_handle* h, int r, EngineStats* es, std::vector<uint64_t> cnt[PU_MAX_LEVELS + 2],
                  std::vector<uint32_t> alive[PU_MAX_LEVELS + 2]) {
+    int qrc = resident_quiesce(h);
+    if (qrc) return qrc;
     const Geo& g = h->geo;
     char* base = h->arena + (size_t)r * g.replica_bytes;
     HIP_TRY(hipStreamSynchronize(h->stream), PU_EIO);
@@ -536,6 +717,29 @@ int pu_config_jit_warm(const pu_sim_cfg* cfg) {
     return pu::jit_warm(geo, nullptr);
 }
 
+int pu_set_resident(pu_handle* h, int mode) {
+    if (!h || mode < -1 || mode > 1) return pu::set_error(PU_EINVAL, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    const int prev = h->res.mode;
+    if (mode == 0) {
+        int rc = resident_stop(h);
+        if (rc) return rc;
+    }
+    if (mode >= 0) h->res.mode = mode;
+    return prev;
+}
+
+int pu_resident_info(pu_handle* h, uint64_t* out4) {
+    if (!h || !out4) return pu::set_error(PU_EINVAL, "bad arguments");
+    std::lock_guard<std::mutex> lk(h->mu);
+    const bool live = h->res.running && h->res.mb && !((volatile PuMailbox*)h->res.mb)->d.exited;
+    out4[0] = live ? 1 : 0;
+    out4[1] = h->res.commands;
+    out4[2] = h->res.launches;
+    out4[3] = resident_eligible(h, 1) ? 1 : 0;
+    return 0;
+}
+
 int pu_compiled_config(const pu_handle* h) { return h && h->jit.ok ? (h->jit_throughput ? 2 : 1) : 0; }
 int pu_compiled_compiler(const pu_handle* h) {
     if (!h || !h->jit.ok) return 0;
@@ -603,6 +807,11 @@ pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device) {
         const char* e = std::getenv("PRIMEUNCORE_LDS_HEADERS");
         h->lds_headers_ok = geo.nqueues <= pu_engine_lds_header_queues() && !(e && e[0] == '0');
         h->lds_headers_short = e && e[0] == '2';
+        // resident mode for pu_access / short host batches (on unless "0")
+        const char* r = std::getenv("PRIMEUNCORE_RESIDENT");
+        h->res.mode = r && r[0] == '0' ? 0 : 1;
+        const char* idle = std::getenv("PRIMEUNCORE_RESIDENT_IDLE_MS");
+        if (idle && std::atof(idle) > 0) h->res.idle_ticks = (uint64_t)(std::atof(idle) * 1e5);
     }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream create failed");
     if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) return fail("event create failed");
@@ -662,6 +871,7 @@ pu_handle* pu_create(const pu_sim_cfg* cfg, int num_replicas, int device) {
 
 void pu_destroy(pu_handle* h) {
     if (!h) return;
+    resident_free(h);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->arena) (void)hipFree(h->arena);
     if (h->d_geo) (void)hipFree(h->d_geo);
@@ -676,6 +886,8 @@ void pu_destroy(pu_handle* h) {
 int pu_reset(pu_handle* h) {
     if (!h) return pu::set_error(PU_EINVAL, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);
+    int rc = resident_stop(h);
+    if (rc) return rc;
     return reset_state(h);
 }
 
@@ -796,6 +1008,14 @@ int access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n, int32_
     if (replica < 0 || replica >= h->R) return pu::set_error(PU_ERANGE, "replica out of range");
     if (n == 0) return 0;
     std::lock_guard<std::mutex> lk(h->mu);
+    if (resident_eligible(h, n)) {
+        // no launch: the resident kernel (headers already in its CU's LDS)
+        const uint32_t flags = (extra & PU_KF_NOHALT) ? extra : (h->replay_flags | extra);
+        uint64_t err = 0;
+        int rrc = resident_run(h, replica, reqs, n, flags, delay_out, &err, last_addr);
+        if (rrc) return rrc;
+        return limit_error(err, replica);
+    }
     int rc = ensure_stage(h, n);
     if (rc) return rc;
     // one host-to-device copy of [offsets | requests] from pinned memory
@@ -901,6 +1121,8 @@ int pu::limit_positions(pu_handle* h, uint64_t* out, size_t n) {
     if (!h || (!out && n)) return pu::set_error(PU_EINVAL, "bad arguments");
     if (n > (size_t)h->R) return pu::set_error(PU_ERANGE, "more replicas than the handle holds");
     if (n == 0) return 0;
+    int rrc = resident_stop(h);
+    if (rrc) return rrc;
     const Geo& g = h->geo;
     HIP_TRY(hipStreamSynchronize(h->stream), PU_EIO);
     HIP_TRY(hipMemcpy2D(out, sizeof(uint64_t), h->arena + g.off_run + offsetof(RunState, limit_at), g.replica_bytes,
@@ -951,6 +1173,8 @@ int pu_run_device_pool(pu_handle* h, const pu_req* d_reqs, const uint64_t* d_off
 
 int pu_synchronize(pu_handle* h) {
     if (!h) return pu::set_error(PU_EINVAL, "null handle");
+    int qrc = resident_quiesce(h);   // a device-wide wait would otherwise last until the resident kernel idles out
+    if (qrc) return qrc;
     HIP_TRY(hipDeviceSynchronize(), PU_EIO);
     float ms = 0;
     if (hipEventElapsedTime(&ms, h->ev0, h->ev1) == hipSuccess) h->last_ms = ms;
@@ -970,6 +1194,8 @@ int pu_core_completion(pu_handle* h, int replica, int64_t* out, size_t n) {
     if (!h || !out) return pu::set_error(PU_EINVAL, "bad arguments");
     if (replica < 0 || replica >= h->R) return pu::set_error(PU_ERANGE, "replica out of range");
     size_t k = n < (size_t)h->geo.num_cores ? n : (size_t)h->geo.num_cores;
+    int qrc = resident_quiesce(h);
+    if (qrc) return qrc;
     std::vector<int64_t> tmp((size_t)h->geo.num_cores);
     char* base = h->arena + (size_t)replica * h->geo.replica_bytes;
     HIP_TRY(hipStreamSynchronize(h->stream), PU_EIO);

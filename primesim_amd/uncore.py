@@ -89,6 +89,8 @@ def lib() -> C.CDLL:
         "pu_stats_get": (C.c_int, [C.c_void_p, C.c_int, P(A.Stats)]),
         "pu_report": (C.c_long, [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_size_t]),
         "pu_last_kernel_ms": (C.c_double, [C.c_void_p]),
+        "pu_set_resident": (C.c_int, [C.c_void_p, C.c_int]),
+        "pu_resident_info": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
         "pu_last_error": (C.c_char_p, []),
         "pu_version": (C.c_char_p, []),
         "pu_set_replay_mode": (C.c_int, [C.c_void_p, C.c_int]),
@@ -528,6 +530,21 @@ class UncoreManager:
 
     def last_kernel_ms(self) -> float:
         return float(lib().pu_last_kernel_ms(self._handle()))
+
+    def set_resident(self, mode: int) -> int:
+        """Resident mode for uncore_access / short batches (pu_set_resident):
+        1 on, 0 off, -1 query; returns the previous mode."""
+        rc = lib().pu_set_resident(self._handle(), mode)
+        if rc < 0:
+            raise UncoreError(last_error())
+        return rc
+
+    def resident_info(self) -> dict:
+        """{running, commands, launches, eligible} of the resident kernel (pu_resident_info)."""
+        out = (C.c_uint64 * 4)()
+        if lib().pu_resident_info(self._handle(), out) != 0:
+            raise UncoreError(last_error())
+        return {"running": bool(out[0]), "commands": int(out[1]), "launches": int(out[2]), "eligible": bool(out[3])}
 
     def stats(self, replica: int = 0) -> A.Stats:
         s = A.Stats()

@@ -8,6 +8,7 @@
 # Steps:
 #   tests        pytest -m gpu (the whole GPU parity suite)
 #   smoke        __graft_entry__.smoke()
+#   latency      tools/latency_bench.py: uncore_access and one message per call, resident kernel vs a launch per call
 #   traffic      PMC fabric traffic of the headline kernel on the driver's window (tools/pmc_traffic.py)
 #   bench        bench.py on the driver's config (--steps 20 --warmup 5), carrying TAG_traffic.json if present
 #   bench_default  bench.py with no flags
@@ -17,6 +18,8 @@
 #   sq_single    the same for one simulation alone, open loop and closed loop (latency kernel)
 #   handoff      tools/probe/handoff: dependent hand-off latency between two waves
 #   tworank      bench.py --gpus 2 with both ranks on card 0 (gloo)
+#   sweep        tools/relax/sweep_bench: one relaxation sweep's phases L and F on the GPU, W = 1,024 and 4,096
+#                (inputs from tools/relax/make_sweeps.sh), plus its rocprofv3 kernel stats
 #   tworank_parity  the same with each rank's reference parity processes and the job-level roofline
 #   regions_single  lone-wave region profiles of the shipped compiled-configuration latency kernel
 #                (-DPU_PROF through PRIMEUNCORE_JIT_EXTRA), open and closed loop
@@ -71,7 +74,8 @@ ab() {   # ab ROUNDS MODES VARIANTS
 for S in "$@"; do
   echo "[gpu_session] $T: $S ($(date +%T))"
   case $S in
-    tests) timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > ${O}_gpu_tests.log 2>&1 || exit 1;;
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > ${O}_gpu_tests.log 2>&1 || exit 1;;
+    latency) timeout -k 10 300 python tools/latency_bench.py --calls 2000 --out ${O}_latency.json > ${O}_latency.log 2>&1 || exit 1;;
     smoke) timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > ${O}_smoke.log 2>&1 || exit 1;;
     traffic) timeout -k 10 500 python tools/pmc_traffic.py --work /tmp/pmc --out ${O}_traffic.json -- $DRIVER --no-cpu --no-extras > ${O}_traffic.log 2>&1 || exit 1;;
     bench) TJ=""; [ -f ${O}_traffic.json ] && TJ="--traffic-json ${O}_traffic.json"
@@ -88,6 +92,11 @@ for S in "$@"; do
     handoff) timeout -k 10 120 tools/probe/handoff > ${O}_handoff.json 2> ${O}_handoff.log || exit 1;;
     tworank) PU_BENCH_DEVICE=0 timeout -k 10 300 $BENCH --gpus 2 --steps 3 --warmup 2 --no-cpu --dist-backend gloo > ${O}_two_rank.json 2> ${O}_two_rank.log || exit 1;;
     tworank_parity) PU_BENCH_DEVICE=0 timeout -k 10 400 $BENCH --gpus 2 --steps 3 --warmup 2 --dist-backend gloo > ${O}_two_rank_parity.json 2> ${O}_two_rank_parity.log || exit 1;;
+    sweep) for W in 1024 4096; do
+             timeout -k 10 120 tools/relax/sweep_bench tools/relax/data/w$W 200 > ${O}_sweep_w$W.json 2> ${O}_sweep_w$W.log || exit 1
+           done
+           timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/${T}_sweep -o run -- tools/relax/sweep_bench tools/relax/data/w4096 50 > ${O}_sweep_w4096_rocprof.json 2> ${O}_sweep_rocprof.log || exit 1
+           cp /tmp/${T}_sweep/run_kernel_stats.csv ${O}_sweep_kernel_stats.csv || exit 1;;
     regions_single)
       timeout -k 10 200 python tools/prof_regions.py --jit -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras > ${O}_regions_single_open.txt 2>&1 || exit 1
       timeout -k 10 200 python tools/prof_regions.py --jit -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras --replay closed > ${O}_regions_single_closed.txt 2>&1 || exit 1;;

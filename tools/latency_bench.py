@@ -1,8 +1,9 @@
 """Latency of the single-request and per-message paths (run on the GPU box).
 
-uncore_access (pu_access: one launch per request) and access_batch of one
-100-request message (pu_access_batch: one launch per message, prime.cpp's
-MEM_REQUESTS), on replica 0 of a C4 engine after a warm-up, wall-clock per call.
+uncore_access (pu_access) and access_batch of one 100-request message
+(pu_access_batch, prime.cpp's MEM_REQUESTS), on replica 0 of a C4 engine after a
+warm-up, wall-clock per call; with the resident kernel (no launch per call) and
+with one launch per call (pu_set_resident 0), each on its own slice of the stream.
 
     python tools/latency_bench.py [--calls 2000] [--out gpurun_out/latency.json]
 """
@@ -22,6 +23,8 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=2000)
     ap.add_argument("--out", default="")
+    ap.add_argument("--resident", choices=("0", "1", "both"), default="both",
+                    help="resident mode (pu_set_resident) on, off, or both in turn (each on its own slice of the stream)")
     a = ap.parse_args()
     import primesim_amd as P
     from primesim_amd import _abi as A
@@ -34,7 +37,22 @@ def main() -> None:
     for prog, th in P.stream_threads(spec):
         um.allocCore(prog, th)
     um.access_batch(reqs[:100_000])                    # warm caches and link histories
-    i0 = 100_000
+    out = {}
+    for mode in ((1, 0) if a.resident == "both" else (int(a.resident),)):
+        um.set_resident(mode)
+        out["resident" if mode else "launch_per_call"] = measure(um, reqs, a, 100_000 + (0 if mode else 10 * a.calls))
+    res = {"library_source_hash": P.uncore.library_source_hash(), "calls": a.calls,
+           "lds_headers_env": os.environ.get("PRIMEUNCORE_LDS_HEADERS", ""), **out,
+           "resident_info": um.resident_info()}
+    print(json.dumps(res))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+    um.close()
+
+
+def measure(um, reqs, a, i0: int) -> dict:
+    import primesim_amd as P
     t0 = time.perf_counter()
     for q in reqs[i0:i0 + a.calls]:
         ins = P.InsMem(mem_type=int(q["mem_type"]), prog_id=int(q["prog_id"]), addr_dmem=int(q["addr"]))
@@ -52,10 +70,8 @@ def main() -> None:
     per_msg = (time.perf_counter() - t0) / nmsg
     n = sum(e - s for s, e in bounds)
     res = {"uncore_access_us": single * 1e6, "message_us": per_msg * 1e6, "requests_per_message": n / nmsg,
-           "message_us_per_request": per_msg * 1e6 / (n / nmsg), "calls": a.calls,
-           "kernel_us_per_message": kms * 1e3 / nmsg,
-           "lds_headers_env": os.environ.get("PRIMEUNCORE_LDS_HEADERS", ""),
-           "library_source_hash": P.uncore.library_source_hash()}
+           "message_us_per_request": per_msg * 1e6 / (n / nmsg),
+           "kernel_us_per_message": kms * 1e3 / nmsg}
     # kernel time per request against the launch size (contiguous slices of the
     # same stream): separates per-launch costs from the per-request chain
     pos = bounds[-1][1]
@@ -69,11 +85,7 @@ def main() -> None:
                             "wall_us_per_request": wall * 1e6 / (e - pos)}
         pos = e
     res["size_sweep"] = sweep
-    print(json.dumps(res))
-    if a.out:
-        with open(a.out, "w") as f:
-            json.dump(res, f, indent=1)
-    um.close()
+    return res
 
 
 if __name__ == "__main__":

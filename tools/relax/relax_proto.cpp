@@ -22,6 +22,16 @@
 //
 // usage: relax_proto PREFIX N_CORES WINDOW [max_sweeps] [guess mode 0|1] [bands]
 // (bands > 0: print the home-tile band statistics of the first sweep and exit)
+// Environment (the GPU sweep measurement, tools/relax/sweep_bench.hip):
+//   RELAX_SKIP=K        run the first K requests exactly (sequentially, checked
+//                       against PREFIX.delay) before the first window
+//   RELAX_DUMP=DIR      relax ONE window after the skip and, at sweep
+//   RELAX_DUMP_SWEEP=S  S (default 2), write phase L's input (every link's
+//                       window-start state and its visits in canonical order,
+//                       with the exact delays this sweep's fold produced) and
+//                       phase F's input (the window's home-slice events in
+//                       canonical order, the window-start lines of every home
+//                       set they touch, and the outcome of each) to DIR
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -180,8 +190,25 @@ struct Prog {
 };
 
 // ---- F: functional fold with given stamps (stampL[r] = L1 stamp, stampH[r] = home stamp)
+// One home-slice access of phase F (home_access), as the GPU sweep replays it.
+struct HomeEv {
+    uint32_t slot;       // (home, set) slot of the dump
+    uint32_t type;       // 0 RD, 1 WR, 2 WB
+    int32_t prog, cid;
+    uint64_t tag;
+    int64_t stamp;
+    int32_t way;         // outcome: the way the access used
+    uint32_t fstate;     // outcome: the line's state after it
+};
+
 struct Functional {
     FState s;
+    // exact mode: the line the request's home access stamped (patched with the
+    // home arrival once the request transmit is timed)
+    Cache* last_home = nullptr;
+    long last_li = -1;
+    std::vector<HomeEv>* rec = nullptr;         // phase F events, when recording
+    std::vector<std::pair<int, uint64_t>>* rec_set = nullptr;   // per event (home, set)
     long lookup(Cache& c, int sets, int ways, int idxb, uint64_t addr, int prog) {
         uint64_t set = (addr >> C.off) % (uint64_t)sets, tg = addr >> (C.off + idxb);
         size_t b0 = c.base(set);
@@ -289,6 +316,14 @@ struct Functional {
         uint8_t fs = d.st[li];
         *out = fs == B ? S : fs;
         d.ts[li] = stamp;
+        last_home = &d;
+        last_li = li;
+        if (rec) {
+            const uint64_t set = (addr >> C.off) % (uint64_t)C.d_sets;
+            rec->push_back({0, (uint32_t)type, prog, cid, addr >> (C.off + C.d_idx), stamp,
+                            (int32_t)(li - (long)d.base(set)), fs});
+            rec_set->push_back({h, set});
+        }
     }
     // mesi_directory at L1 (the last level)
     void access(const Req& q, int64_t stampL, int64_t stampH, Prog& P) {
@@ -380,6 +415,82 @@ struct Walker {
     }
 };
 
+// Exact sequential execution (the reference's order, live link queues): the
+// fast-forward to the measured window.
+struct Exact {
+    std::vector<Queue>* links;
+    uint64_t walk(int src, int dst, int len, uint64_t start) {
+        if (src == dst) return 0;
+        int plen = C.hdr + (int)std::ceil((double)len / C.width);
+        int sx = src % C.w, sy = src / C.w, rx = dst % C.w, ry = dst / C.w;
+        uint64_t t = start + C.inject;
+        auto hop = [&](int d) {
+            t += C.router;
+            bool mg;
+            t += queue_delay((*links)[link_index(sx, sy, d)], t, (uint64_t)plen, (uint64_t)C.link, &mg) + C.link;
+        };
+        while (sx != rx) { int d = rx > sx ? 0 : 1; hop(d); sx += d == 0 ? 1 : -1; }
+        while (sy != ry) { int d = ry > sy ? 3 : 2; hop(d); sy += d == 3 ? 1 : -1; }
+        t += C.router;
+        t += (uint64_t)(plen - 1);
+        return t - start;
+    }
+    // one request at running delay D (updated); returns its delay
+    int run(Functional& F, const Req& q, int32_t& D) {
+        if (q.bstart) D = 0;
+        const int64_t T = q.timer + D;
+        Prog P;
+        F.last_home = nullptr;
+        F.access(q, T + C.l1_at, 0, P);   // the home stamp is patched below
+        Cache* hc = F.last_home;
+        const long hli = F.last_li;
+        int d = C.l1_at;
+        if (P.wb_home >= 0) walk(q.core, P.wb_home, C.blk, (uint64_t)(T + d));   // delay discarded (Q3)
+        if (P.kind != 0) {
+            d += (int)walk(q.core, P.home, 0, (uint64_t)(T + d));
+            const int64_t th = T + d;
+            hc->ts[(size_t)hli] = th;
+            int hd = C.d_at;
+            if (P.hp == 1) {
+                hd += (int)walk(P.home, P.owner, 0, (uint64_t)(th + hd));
+                hd += P.owner_at;
+                hd += (int)walk(P.owner, P.home, P.owner_len, (uint64_t)(th + hd));
+            } else if (P.hp == 2) {
+                int pipe = 0, mx = 0;
+                for (const Leg& L : P.legs) {
+                    int tt = pipe;
+                    tt += (int)walk(P.home, L.node, 0, (uint64_t)(th + hd + tt));
+                    tt += L.at;
+                    tt += (int)walk(L.node, P.home, 0, (uint64_t)(th + hd + tt));
+                    mx = std::max(mx, tt);
+                    pipe += C.hdr;
+                }
+                hd += mx;
+            }
+            hd += P.dram_add;
+            d += hd;
+            d += (int)walk(P.home, q.core, P.reply_len, (uint64_t)(T + d));
+        }
+        D += d - 1;
+        return d;
+    }
+};
+
+static void wfile(const std::string& path, const void* p, size_t bytes) {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f || std::fwrite(p, 1, bytes, f) != bytes) { std::fprintf(stderr, "cannot write %s\n", path.c_str()); std::exit(1); }
+    std::fclose(f);
+}
+
+// Phase L's per-link record for the GPU sweep: the window-start state and the
+// range of its visits (l_vis.bin, canonical order).
+struct LinkRec {
+    uint64_t n, newest;
+    double sum, sum_sq;
+    uint32_t nint, vis_begin, vis_end, link;
+};
+struct VisRec { uint64_t t; uint32_t p, pad; };
+
 int main(int argc, char** argv) {
     if (argc < 4) { std::fprintf(stderr, "usage: relax_proto PREFIX N_CORES WINDOW [max_sweeps] [mode]\n"); return 1; }
     std::string pre = argv[1];
@@ -408,7 +519,18 @@ int main(int argc, char** argv) {
     int32_t carryD = 0;   // running delay of a message that spans windows
     size_t mism = 0;
     long total_sweeps = 0, windows = 0, max_s = 0;
-    for (size_t a = 0; a < n; a += W) {
+    const size_t skip = std::min(n, (size_t)std::atol(getenv("RELAX_SKIP") ? getenv("RELAX_SKIP") : "0"));
+    const char* dump_dir = getenv("RELAX_DUMP");
+    const int dump_sweep = getenv("RELAX_DUMP_SWEEP") ? std::atoi(getenv("RELAX_DUMP_SWEEP")) : 2;
+    if (skip) {
+        Exact X{&links};
+        size_t bad = 0;
+        for (size_t i = 0; i < skip; i++) bad += X.run(F, reqs[i], carryD) != want[i];
+        std::printf("exact fast-forward: %zu requests, %zu mismatches\n", skip, bad);
+        if (bad) return 1;
+        mism += bad;
+    }
+    for (size_t a = skip; a < n; a += W) {
         size_t b = std::min(n, a + W), wn = b - a;
         std::vector<int64_t> stampL(wn), stampH(wn);
         // sweep-0 stamp guesses: no delay within messages, zero-load home arrival
@@ -428,7 +550,13 @@ int main(int argc, char** argv) {
             sweep++;
             // F
             F.s = base;
+            std::vector<HomeEv> fev;
+            std::vector<std::pair<int, uint64_t>> fset;
+            const bool dumping = dump_dir && sweep == dump_sweep;
+            if (dumping) { F.rec = &fev; F.rec_set = &fset; }
             for (size_t i = 0; i < wn; i++) F.access(reqs[a + i], stampL[i], stampH[i], progs[i]);
+            F.rec = nullptr;
+            F.rec_set = nullptr;
             // T
             for (auto& v : lv) v.clear();
             for (size_t i = 0; i < wn; i++) { cur[i].clear(); vlink[i].clear(); vp[i].clear(); }
@@ -517,6 +645,71 @@ int main(int argc, char** argv) {
                 }
             }
             if (changed == 0 && stamps_same) done = true;
+            if (dumping) {
+                // ---- phase L: every visited link's window-start state, its visits
+                std::vector<LinkRec> lr;
+                std::vector<uint64_t> liv;      // 128 (first, second) slots per link record
+                std::vector<VisRec> vis;
+                std::vector<uint64_t> qd;
+                for (size_t li = 0; li < nl; li++) {
+                    if (lv[li].empty()) continue;
+                    const Queue& Q = lbase[li];
+                    LinkRec R{Q.n, Q.newest, Q.sum, Q.sum_sq, (uint32_t)Q.iv.size(), (uint32_t)vis.size(), 0,
+                              (uint32_t)li};
+                    for (size_t k = 0; k < 128; k++) {
+                        liv.push_back(k < Q.iv.size() ? Q.iv[k].first : 0);
+                        liv.push_back(k < Q.iv.size() ? Q.iv[k].second : 0);
+                    }
+                    for (auto [r, j] : lv[li]) {
+                        vis.push_back({cur[r][j].t, (uint32_t)vp[r][j], 0});
+                        qd.push_back(cur[r][j].qd);
+                    }
+                    R.vis_end = (uint32_t)vis.size();
+                    lr.push_back(R);
+                }
+                const std::string d = dump_dir;
+                wfile(d + "/l_links.bin", lr.data(), lr.size() * sizeof(LinkRec));
+                wfile(d + "/l_iv.bin", liv.data(), liv.size() * 8);
+                wfile(d + "/l_vis.bin", vis.data(), vis.size() * sizeof(VisRec));
+                wfile(d + "/l_qd.bin", qd.data(), qd.size() * 8);
+                // ---- phase F: home events with their set slots, and the
+                // window-start lines of those sets: {state, prog, tag, ts} x ways
+                // + the sharer bitmaps (nwords u64 per line)
+                std::vector<std::pair<int, uint64_t>> slots;
+                std::vector<uint32_t> fslot;
+                for (auto& hs : fset) {
+                    auto it = std::find(slots.begin(), slots.end(), hs);
+                    if (it == slots.end()) { slots.push_back(hs); it = slots.end() - 1; }
+                    fslot.push_back((uint32_t)(it - slots.begin()));
+                }
+                for (size_t e = 0; e < fev.size(); e++) fev[e].slot = fslot[e];
+                std::vector<uint64_t> lines;    // per slot, per way: st | prog << 8, tag, ts
+                std::vector<uint64_t> shr;
+                for (auto [h, set] : slots) {
+                    Cache& c = base.home[(size_t)h];
+                    const bool have = c.alive && c.slot[set] >= 0;
+                    for (int w = 0; w < C.d_ways; w++) {
+                        const size_t li = have ? (size_t)c.slot[set] + (size_t)w : 0;
+                        lines.push_back(have ? (uint64_t)c.st[li] | ((uint64_t)(uint32_t)c.id[li] << 8) : 0);
+                        lines.push_back(have ? c.tag[li] : 0);
+                        lines.push_back(have ? (uint64_t)c.ts[li] : 0);
+                        for (int k = 0; k < C.nwords; k++) shr.push_back(have ? c.shr[li * C.nwords + k] : 0);
+                    }
+                }
+                wfile(d + "/f_ev.bin", fev.data(), fev.size() * sizeof(HomeEv));
+                wfile(d + "/f_lines.bin", lines.data(), lines.size() * 8);
+                wfile(d + "/f_shr.bin", shr.data(), shr.size() * 8);
+                const uint32_t meta[8] = {(uint32_t)wn, (uint32_t)lr.size(), (uint32_t)vis.size(), (uint32_t)fev.size(),
+                                          (uint32_t)slots.size(), (uint32_t)C.d_ways, (uint32_t)C.nwords,
+                                          (uint32_t)C.link};
+                wfile(d + "/meta.bin", meta, sizeof meta);
+                size_t maxv = 0;
+                for (auto& R : lr) maxv = std::max<size_t>(maxv, R.vis_end - R.vis_begin);
+                std::printf("dump: window [%zu, %zu) sweep %d: %zu links with visits (max %zu visits), %zu visits, "
+                            "%zu home events over %zu sets\n", a, b, sweep, lr.size(), maxv, vis.size(), fev.size(),
+                            slots.size());
+                return 0;
+            }
             if (getenv("RELAX_VERBOSE"))
                 std::printf("  window %zu sweep %d: visits %zu changed %zu stamps_same %d\n", a / W, sweep, visits,
                             changed, (int)stamps_same);
