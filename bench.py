@@ -851,7 +851,17 @@ def main(argv=None) -> None:
                                    f"({'reference uncore compiled from /root/reference/src, no counting wraps' if kind == 'reference' else 'oracle/cpu_ref restatement'}), "
                                    f"{el:.1f} s"}
                 log(f"[bench] closed-loop cpu baseline ({kind}): {n_cpu / el:.0f} accesses/s")
+            c_ms = float(np.mean(C.kern_ms))
+            c_bytes = alg_bytes(C.delta, cfg) / C.steps
             closed = {"value": C.processed / C.elapsed, "unit": "accesses/s", "steps": C.steps,
+                      "roofline": {"bound": "hbm", "achieved": c_bytes / (c_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+                                   "unit": "GB/s", "frac": c_bytes / (c_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                                   "alg_bytes_per_launch": c_bytes, "avg_launch_ms": c_ms,
+                                   "alg_bytes_per_access": alg_bytes(C.delta, cfg) / max(1, C.processed),
+                                   "tree_visits_per_access": (C.delta["net_distance"] - C.delta["mg1_calls"]) /
+                                                             max(1, C.processed),
+                                   "note": "the closed-loop pass's algorithmic bytes per launch / its HIP-event mean "
+                                           "launch time (same kernel as the headline)"},
                       "per_simulation_accesses_per_s": C.processed / C.elapsed / D.slots,
                       "replica_pool": C.pool,
                       "halted_replicas": C.halted,

@@ -15,6 +15,8 @@
 #   bench_c3 / bench_c5  bench.py --config C3 / C5 on the driver's window (C5 closed loop by default)
 #   rocprof      rocprofv3 --kernel-trace --stats of the driver's config (headline only)
 #   sq           SQ wave-state / instruction counters of the headline kernel (tools/pmc_sq.py)
+#   sq_closed / traffic_closed / regions_closed  the headline kernel's SQ counters, fabric traffic and region
+#                profile on the closed-loop replay of the same workload (bench --replay closed)
 #   sq_single    the same for one simulation alone, open loop and closed loop (latency kernel)
 #   handoff      tools/probe/handoff: dependent hand-off latency between two waves
 #   tworank      bench.py --gpus 2 with both ranks on card 0 (gloo)
@@ -87,6 +89,9 @@ for S in "$@"; do
              timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/${T}_prof -o run -- python3 bench.py $DRIVER --no-cpu --no-extras $TJ > ${O}_bench_under_rocprof.json 2> ${O}_rocprof.log || exit 1
              cp /tmp/${T}_prof/run_kernel_stats.csv ${O}_kernel_stats.csv || exit 1;;
     sq) timeout -k 10 700 python tools/pmc_sq.py --work /tmp/pmc_sq --out ${O}_sq.json -- --steps 3 --warmup 5 --no-cpu --no-extras > ${O}_sq.log 2>&1 || exit 1;;
+    sq_closed) timeout -k 10 700 python tools/pmc_sq.py --work /tmp/pmc_sqc --out ${O}_sq_closed.json -- --steps 3 --warmup 5 --no-cpu --no-extras --replay closed > ${O}_sq_closed.log 2>&1 || exit 1;;
+    traffic_closed) timeout -k 10 500 python tools/pmc_traffic.py --work /tmp/pmcc --out ${O}_traffic_closed.json -- $DRIVER --no-cpu --no-extras --replay closed > ${O}_traffic_closed.log 2>&1 || exit 1;;
+    regions_closed) timeout -k 10 300 python tools/prof_regions.py --jit -- --steps 3 --warmup 5 --no-cpu --no-extras --replay closed > ${O}_regions_closed.txt 2>&1 || exit 1;;
     sq_single) timeout -k 10 500 python tools/pmc_sq.py --kernel pu_jit_uncore_s1_h1 --work /tmp/pmc_sq1 --out ${O}_sq_single_open.json -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras > ${O}_sq_single_open.log 2>&1 || exit 1
                timeout -k 10 500 python tools/pmc_sq.py --kernel pu_jit_uncore_s1_h1 --work /tmp/pmc_sq2 --out ${O}_sq_single_closed.json -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras --replay closed > ${O}_sq_single_closed.log 2>&1 || exit 1;;
     handoff) timeout -k 10 120 tools/probe/handoff > ${O}_handoff.json 2> ${O}_handoff.log || exit 1;;

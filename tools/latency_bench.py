@@ -24,7 +24,7 @@ def main() -> None:
     ap.add_argument("--calls", type=int, default=2000)
     ap.add_argument("--out", default="")
     ap.add_argument("--resident", choices=("0", "1", "both"), default="both",
-                    help="resident mode (pu_set_resident) on, off, or both in turn (each on its own slice of the stream)")
+                    help="resident mode (pu_set_resident) on, off, or both in turn (each on a fresh engine over the same slices)")
     a = ap.parse_args()
     import primesim_amd as P
     from primesim_amd import _abi as A
@@ -32,23 +32,49 @@ def main() -> None:
     cfg = P.config_from_dict(CF.preset("C4"))
     spec = P.StreamSpec(A.PU_STREAM_UNIFORM_HOTSPOT, 1024, seed=4, num_quanta=2, max_requests=200_000 + 200 * a.calls)
     reqs = P.generate_stream(spec)
-    um = P.UncoreManager()
-    um.init(cfg, replicas=1)
-    for prog, th in P.stream_threads(spec):
-        um.allocCore(prog, th)
-    um.access_batch(reqs[:100_000])                    # warm caches and link histories
     out = {}
     for mode in ((1, 0) if a.resident == "both" else (int(a.resident),)):
+        # a fresh engine per mode, the same warm-up and the same stream slices:
+        # the per-request work depends on the stream's phase (link histories)
+        um = P.UncoreManager()
+        um.init(cfg, replicas=1)
+        for prog, th in P.stream_threads(spec):
+            um.allocCore(prog, th)
         um.set_resident(mode)
-        out["resident" if mode else "launch_per_call"] = measure(um, reqs, a, 100_000 + (0 if mode else 10 * a.calls))
+        um.access_batch(reqs[:100_000])                # warm caches and link histories (one launch)
+        r = {"call_overhead_us": call_overhead(um, reqs, a.calls)}
+        r.update(measure(um, reqs, a, 100_000))
+        r["resident_info"] = um.resident_info()
+        out["resident" if mode else "launch_per_call"] = r
+        um.close()
     res = {"library_source_hash": P.uncore.library_source_hash(), "calls": a.calls,
-           "lds_headers_env": os.environ.get("PRIMEUNCORE_LDS_HEADERS", ""), **out,
-           "resident_info": um.resident_info()}
+           "lds_headers_env": os.environ.get("PRIMEUNCORE_LDS_HEADERS", ""), **out}
     print(json.dumps(res))
     if a.out:
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)
-    um.close()
+
+
+def call_overhead(um, reqs, calls: int) -> float:
+    """µs per pu_access_status call whose request is an L1 hit (one core
+    re-reading one line, timers advancing): the call's own cost, the
+    simulation work nearly nil.  The ctypes call is prepared once."""
+    import ctypes as C
+
+    import primesim_amd as P
+    q = reqs[100_000]
+    core, prog, t0 = int(q["core"]), int(q["prog_id"]), int(q["timer"])
+    addr = C.c_uint64(int(q["addr"]))
+    d = C.c_int32(0)
+    f, h = P.uncore.lib().pu_access_status, um._handle()
+    for k in range(10):                                # the line into the L1
+        addr.value = int(q["addr"])
+        f(h, core, prog, 0, C.byref(addr), t0 + k, C.byref(d))
+    t = time.perf_counter()
+    for k in range(calls):
+        addr.value = int(q["addr"])
+        f(h, core, prog, 0, C.byref(addr), t0 + 10 + k, C.byref(d))
+    return (time.perf_counter() - t) / calls * 1e6
 
 
 def measure(um, reqs, a, i0: int) -> dict:
