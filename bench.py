@@ -78,18 +78,20 @@ METRIC = "simulated memory accesses/sec (uncore) at 1024 cores; % HBM roofline"
 # configuration (BASELINE.json configs[3]); C3 and C5 are the deeper and the
 # larger shapes, measured the same way (their lines name their own metric).
 WORKLOADS = {
-    "C3": {"cores": 256, "stream": "PU_STREAM_MULTIPROGRAM", "num_progs": 4, "replay": "open",
+    # (C3's replicas run ~2x faster than C4's: twice the chunk, so the timed
+    # window outlasts the 20 slices and the pool never runs dry)
+    "C3": {"cores": 256, "stream": "PU_STREAM_MULTIPROGRAM", "num_progs": 4, "replay": "open", "chunk": 81920,
            "desc": "C3: 256-core 16x16 mesh, private L1 32KB/8W + private L2 256KB/8W/5cyc + 1MB/16W shared-LLC "
                    "slice per tile, directory MESI full-map; multi-programmed mix, 4 programs x 64 cores, "
                    "per-program footprints 4-64 MB, 20% writes"},
-    "C4": {"cores": 1024, "stream": "PU_STREAM_UNIFORM_HOTSPOT", "num_progs": 1, "replay": "open",
+    "C4": {"cores": 1024, "stream": "PU_STREAM_UNIFORM_HOTSPOT", "num_progs": 1, "replay": "open", "chunk": 40960,
            "desc": "C4: 1024-core 32x32 mesh, L1 32KB/8W + 256KB/8W shared-LLC slice per tile, "
                    "directory MESI full-map, uniform 2^20 lines + 64-line hotspot, 25% writes"},
     # open loop, the producer/consumer stream's link delays pass 2^31 within
     # its first quantum (golden big_c5_preset stops at request 165,860 by
     # prime.cpp:130-134): every replica would halt in the warm-up, so C5 is
     # replayed closed loop (core_manager.cpp:265) by default
-    "C5": {"cores": 4096, "stream": "PU_STREAM_PRODUCER_CONSUMER", "num_progs": 1, "replay": "closed",
+    "C5": {"cores": 4096, "stream": "PU_STREAM_PRODUCER_CONSUMER", "num_progs": 1, "replay": "closed", "chunk": 40960,
            "desc": "C5: 4096-core 64x64 mesh, L1 32KB/8W + 256KB/8W shared-LLC slice per tile, directory MESI "
                    "full-map; producer/consumer pairs (p, p+2048) sharing 1,024-line buffers, 50% writes"},
 }
@@ -648,7 +650,8 @@ def parse_args(argv=None):
                     help="wavefront slots per GPU (0 = every replica slot the kernel keeps resident)")
     ap.add_argument("--spare-replicas", type=float, default=0.1,
                     help="replicas beyond the resident wavefront slots, as a fraction of them (replica pool)")
-    ap.add_argument("--chunk", type=int, default=40960, help="requests per replica per step")
+    ap.add_argument("--chunk", type=int, default=0,
+                    help="requests per replica per step (0 = the configuration's: 40,960 for C4 and C5, 81,920 for C3)")
     ap.add_argument("--slice-ms", type=float, default=400.0,
                     help="timed steps are wall-time slices: every replica continues its own stream for this long "
                          "per launch (stopping only between requests); 0 = fixed --chunk requests per replica per step")
@@ -675,6 +678,8 @@ def parse_args(argv=None):
     a = ap.parse_args(argv)
     if a.replay is None:
         a.replay = WORKLOADS[a.config]["replay"]
+    if a.chunk <= 0:
+        a.chunk = WORKLOADS[a.config]["chunk"]
     return a
 
 

@@ -376,10 +376,13 @@ int pu_access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n,
  * process exit.  It needs the compiled configuration and a replica whose queue
  * headers fit one CU's LDS; otherwise (or with PRIMEUNCORE_RESIDENT=0) every
  * call launches as before.  pu_set_resident: mode 1 on, 0 off (joins a running
- * kernel), -1 query; returns the previous mode.  pu_resident_info writes
- * {kernel running, commands served, kernels launched, eligible}. */
+ * kernel), -1 query; returns the previous mode.  pu_resident_info writes up
+ * to n of {kernel running, commands served, kernels launched, eligible, then
+ * summed over the commands: the kernel's request-copy, message-loop, close
+ * (run state and counters) and mailbox phases in 10-ns ticks, and the host's
+ * post-to-answer time in ns} and returns how many it wrote. */
 int pu_set_resident(pu_handle* h, int mode);
-int pu_resident_info(pu_handle* h, uint64_t* out4);
+int pu_resident_info(pu_handle* h, uint64_t* out, size_t n);
 
 /* Batch path from device memory, all replicas at once, asynchronous on
  * `hip_stream` (a hipStream_t; NULL = the engine's own stream, see

@@ -142,7 +142,10 @@ constexpr bool kWideSets = true;
 constexpr bool kWideSets = false;
 #endif
 
-// A queue's ring as held by the wave: physical slots lane and lane+64.
+// A queue's ring as held by the wave, in logical order: lane l holds the
+// live intervals l and l+64 counted from the ring cursor (physical slots
+// (head + l) & 127 and (head + 64 + l) & 127), so the search's hit mask needs no
+// rotation and an edit's index ranges no wrap against the cursor.
 struct RingView {
     uint64_t lf, ls, hf, hs;
 };
@@ -192,7 +195,12 @@ constexpr int ring_pf() { return LH ? PU_RING_PF : PU_RING_PF_TP; }
 #define PU_WAVES_1LEVEL 5
 #endif
 #endif
-#define PU_MIN_WAVES(NL) ((NL) == 1 ? PU_WAVES_1LEVEL : 1)
+// Deeper hierarchies (NL > 1): the compiler's choice unless PU_WAVES_DEEP is
+// set (tools/gpu_session.sh V@-DPU_WAVES_DEEP=W A/Bs of bench --config C3).
+#ifndef PU_WAVES_DEEP
+#define PU_WAVES_DEEP 1
+#endif
+#define PU_MIN_WAVES(NL) ((NL) == 1 ? PU_WAVES_1LEVEL : PU_WAVES_DEEP)
 // native vectors (not classes), so loads/stores through global-address-space
 // pointers need no conversion: slot = {first, second}, header = 10 dwords
 typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
@@ -380,19 +388,20 @@ __device__ __forceinline__ AS1 v4u32* q_hdr_c(const NetCtx& c, int q) {
     return reinterpret_cast<AS1 v4u32*>(c.qhdr + c.hdr_c + (uint64_t)q * PU_HDR_C);
 }
 
-// Load the `cnt` live slots of ring q starting at `head` (lane l holds slots l
-// and l+64); dead slots are not fetched and read as 0.
+// Load the `cnt` live slots of ring q starting at `head` in logical order
+// (lane l holds intervals l and l+64); dead intervals are not fetched and
+// read as 0.
 __device__ __forceinline__ void ring_load(const NetCtx& c, int q, uint32_t head, uint32_t cnt, RingView& v) {
     const AS1 v2u64* R = q_ring(c, q);
-    const int ln = lane_id();
+    const uint32_t ln = (uint32_t)lane_id();
     v = RingView{0, 0, 0, 0};
-    if ((((uint32_t)ln - head) & (PU_QRING - 1)) < cnt) {
-        v2u64 a = R[ln];
+    if (ln < cnt) {
+        v2u64 a = R[(head + ln) & (PU_QRING - 1)];
         v.lf = a.x;
         v.ls = a.y;
     }
-    if ((((uint32_t)ln + 64 - head) & (PU_QRING - 1)) < cnt) {
-        v2u64 b = R[ln + 64];
+    if (ln + 64 < cnt) {
+        v2u64 b = R[(head + 64 + ln) & (PU_QRING - 1)];
         v.hf = b.x;
         v.hs = b.y;
     }
@@ -553,32 +562,23 @@ __device__ __forceinline__ uint64_t tree_case(uint64_t f, uint64_t s, uint64_t t
 
 // Tree branch of QueueModelHistoryTree::computeQueueDelay
 // (queue_model_history_tree.cpp:64-112) on the full ring, branch-light: every
-// lane evaluates the search predicate and the outcome for its two slots, the
-// leftmost hit in ring order from `head` is picked with one 128-bit scan, and
-// the edit is one range move (DPP rotate) plus at most two overridden fields.
-// head/cnt are the post-prune values and are updated; edited slots are
-// written back.  The ring side that moves is the shorter one (a prefix move
-// shifts `head`): only the logical order is observable.
+// lane evaluates the search predicate and the outcome for its two intervals
+// (the view is in logical order, RingView), the leftmost hit is picked with
+// one 128-bit scan, and the edit is one range move (DPP rotate) plus at most
+// two overridden fields.  head/cnt are the post-prune values and are updated;
+// edited slots are written back.  The ring side that moves is the shorter one
+// (a prefix move shifts `head`): only the logical order is observable.
 __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingView& v, uint32_t& head,
                                             uint32_t& cnt, uint64_t t, uint64_t p, uint64_t minp, uint64_t& err,
                                             uint64_t& f0n, uint64_t& f1n) {
     const int ln = lane_id();
     PROF_T(p_s);
     const uint64_t tp = t + p;
-    const uint32_t jl = ((uint32_t)ln - head) & (PU_QRING - 1);
-    const uint32_t jh = ((uint32_t)ln + 64 - head) & (PU_QRING - 1);
+    const uint32_t head0 = head;
+    const uint32_t jl = (uint32_t)ln, jh = (uint32_t)ln + 64;   // logical indices of the lane's intervals
     const bool pl = jl < cnt && ((v.lf <= t && tp <= v.ls) || (t < v.lf && v.ls - v.lf >= p));
     const bool ph = jh < cnt && ((v.hf <= t && tp <= v.hs) || (t < v.hf && v.hs - v.hf >= p));
-    uint64_t ml = ballot(pl), mh = ballot(ph);
-    // logical order: rotate the 128-bit hit mask right by head
-    const uint32_t hsh = head & 63;
-    if (head >= 64) {
-        const uint64_t x = ml;
-        ml = mh;
-        mh = x;
-    }
-    const uint64_t rlo = hsh ? (ml >> hsh) | (mh << (64 - hsh)) : ml;
-    const uint64_t rhi = hsh ? (mh >> hsh) | (ml << (64 - hsh)) : mh;
+    const uint64_t rlo = ballot(pl), rhi = ballot(ph);
     uint32_t k;
     if (rlo) k = (uint32_t)__builtin_ctzll(rlo);
     else if (rhi) k = 64 + (uint32_t)__builtin_ctzll(rhi);
@@ -586,13 +586,12 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
         err |= PU_ERRF_QUEUE;
         k = 0;
     }
-    const uint32_t slot = (head + k) & (PU_QRING - 1);
     PROF_ADD(PF_T_SEARCH, p_s);
     PROF_T(p_d);
     // the outcome for the found interval only, on the scalar unit
-    const bool hi_half = slot >= 64;
-    const uint64_t sf = rl64(hi_half ? v.hf : v.lf, (int)(slot & 63));
-    const uint64_t ss = rl64(hi_half ? v.hs : v.ls, (int)(slot & 63));
+    const bool hi_half = k >= 64;
+    const uint64_t sf = rl64(hi_half ? v.hf : v.lf, (int)(k & 63));
+    const uint64_t ss = rl64(hi_half ? v.hs : v.ls, (int)(k & 63));
     uint32_t op;
     const uint64_t d = tree_case(sf, ss, t, p, minp, op);
     // the edit as: slots whose logical index is in [r0, r0+rlen) take their
@@ -654,10 +653,11 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
     PROF_ADD(PF_T_EDIT, p_e);
     PROF_T(p_w);
     AS1 v2u64* R = q_ring(c, q);
-    if (wl) R[ln] = v2u64{lf, ls};
-    if (wh) R[ln + 64] = v2u64{hf, hs};
-    // the header's copies of the first two interval starts
-    const uint32_t s0 = head, s1 = (head + 1) & (PU_QRING - 1);
+    if (wl) R[(head0 + jl) & (PU_QRING - 1)] = v2u64{lf, ls};
+    if (wh) R[(head0 + jh) & (PU_QRING - 1)] = v2u64{hf, hs};
+    // the header's copies of the first two interval starts: the new cursor is
+    // the old logical index (head - head0) & 127 (0, 1 or 127)
+    const uint32_t s0 = (head - head0) & (PU_QRING - 1), s1 = (s0 + 1) & (PU_QRING - 1);
     f0n = rl64(s0 < 64 ? lf : hf, (int)(s0 & 63));
     f1n = rl64(s1 < 64 ? lf : hf, (int)(s1 & 63));
     PROF_ADD(PF_T_STORE, p_w);
@@ -934,14 +934,16 @@ __device__ __forceinline__ v2u64* ring_slot(int slot) {
     else return lds_ring_tp[slot];
 }
 
-// Stage ring q (live slots [head, head+cnt)) into LDS slot `slot`; dead slots
-// read the head slot instead (one shared line) and are never used.
+// Stage ring q (live slots [head, head+cnt)) into LDS slot `slot` in logical
+// order; dead positions read the head slot instead (one shared line) and are
+// never used.
 template <bool LH>
 __device__ __forceinline__ void ring_dma(const NetCtx& c, int q, uint32_t head, uint32_t cnt, int slot) {
     const int ln = lane_id();
     const AS1 v2u64* R = q_ring(c, q);
-    const AS1 v2u64* ga = R + ((((uint32_t)ln - head) & (PU_QRING - 1)) < cnt ? (uint32_t)ln : head);
-    const AS1 v2u64* gb = R + ((((uint32_t)ln + 64 - head) & (PU_QRING - 1)) < cnt ? (uint32_t)ln + 64 : head);
+    // logical order (RingView): LDS position l <- interval l from the cursor
+    const AS1 v2u64* ga = R + ((uint32_t)ln < cnt ? (head + (uint32_t)ln) & (PU_QRING - 1) : head);
+    const AS1 v2u64* gb = R + ((uint32_t)ln + 64 < cnt ? (head + 64 + (uint32_t)ln) & (PU_QRING - 1) : head);
     const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) v2u64*)ring_slot<LH>(slot);
     const uint32_t lo = __builtin_amdgcn_readfirstlane(la), hi = lo + 64 * sizeof(v2u64);
     unsigned keep;
@@ -2793,6 +2795,7 @@ __device__ __forceinline__ void resident_body(const Geo* __restrict__ g, char* _
             __syncthreads();                          // [D] replica_close
             continue;
         }
+        const uint64_t tk0 = __builtin_amdgcn_s_memrealtime();
         {   // the requests: host mailbox -> device staging, 16 B per lane and step, 4 steps in flight
             AS1 v4u32* dst = (AS1 v4u32*)(AS1 char*)(char*)stage;
             const uint64_t pieces = 2 * n;
@@ -2813,15 +2816,22 @@ __device__ __forceinline__ void resident_body(const Geo* __restrict__ g, char* _
             lds_hq_head = 0;
             lds_main_done = 0;
         }
+        const uint64_t tk1 = __builtin_amdgcn_s_memrealtime();
         replica_loop<NL, false, LH>(e, stage, hdelay, 0, n, nullptr, UINT64_MAX, uni32(lds_res.flags));   // [B]
         if (e.ln == 0) *(volatile AS3 uint32_t*)&lds_main_done = 1u;
+        const uint64_t tk2 = __builtin_amdgcn_s_memrealtime();
         __syncthreads();                              // [C]
         replica_close<NL, LH>(e);                     // [D]
+        const uint64_t tk3 = __builtin_amdgcn_s_memrealtime();
         if (e.ln == 0) {
             lds_res.err |= lds_err;
             volatile PuResDev* Dv = &mb->d;
             Dv->err = lds_res.err;
             Dv->last_addr = lds_eng.last_addr;
+            Dv->phase[0] = (uint32_t)(tk1 - tk0);
+            Dv->phase[1] = (uint32_t)(tk2 - tk1);
+            Dv->phase[2] = (uint32_t)(tk3 - tk2);
+            Dv->phase[3] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tk3);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: delays, counters, run state visible
         if (e.ln == 0) __hip_atomic_store(&mb->d.ack, uni64(lds_res.seq), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -231,7 +231,9 @@ struct PuResDev {           // written by the kernel (its own 64-B line)
     uint64_t err;           // the replica's EngineStats.error_flags after it
     uint64_t last_addr;     // RunState.last_addr after it (TLB translation)
     uint32_t exited, _pad0; // 1 once the kernel has left (stop or idle)
-    uint64_t _pad[4];
+    uint32_t phase[4];      // the command's phases in s_memrealtime ticks (10 ns): request copy,
+                            // replica_loop, replica_close, mailbox writes up to the ack
+    uint64_t _pad[2];
 };
 // Mailbox: {host line, device line}, then pu_req reqs[cap], then int32 delays[cap].
 struct PuMailbox {

@@ -330,6 +330,8 @@ struct pu_handle {
         hipEvent_t after = nullptr; // orders the kernel after the handle's stream
         uint64_t idle_ticks = 5000000;   // 50 ms of s_memrealtime (100 MHz)
         uint64_t commands = 0, launches = 0;
+        uint64_t phase_ticks[4] = {0, 0, 0, 0};   // summed kernel-side phases (PuResDev.phase)
+        uint64_t call_ns = 0;                     // summed host-side post-to-ack time
     } res;
     std::mutex mu;
 };
@@ -541,10 +543,13 @@ int resident_run(pu_handle* h, int replica, const pu_req* reqs, size_t n, uint32
     std::atomic_thread_fence(std::memory_order_acquire);
     R.acked = seq;
     R.commands++;
+    for (int k = 0; k < 4; k++) R.phase_ticks[k] += mb->d.phase[k];
     if (delay_out) std::memcpy(delay_out, (const int32_t*)((const pu_req*)(R.mb + 1) + kResCap), n * sizeof(int32_t));
     *err_out = mb->d.err;
     if (last_addr) *last_addr = mb->d.last_addr;
-    h->last_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    h->last_ms = ms;
+    R.call_ns += (uint64_t)(ms * 1e6);
     return 0;
 }
 
@@ -729,15 +734,15 @@ int pu_set_resident(pu_handle* h, int mode) {
     return prev;
 }
 
-int pu_resident_info(pu_handle* h, uint64_t* out4) {
-    if (!h || !out4) return pu::set_error(PU_EINVAL, "bad arguments");
+int pu_resident_info(pu_handle* h, uint64_t* out, size_t n) {
+    if (!h || (!out && n)) return pu::set_error(PU_EINVAL, "bad arguments");
     std::lock_guard<std::mutex> lk(h->mu);
-    const bool live = h->res.running && h->res.mb && !((volatile PuMailbox*)h->res.mb)->d.exited;
-    out4[0] = live ? 1 : 0;
-    out4[1] = h->res.commands;
-    out4[2] = h->res.launches;
-    out4[3] = resident_eligible(h, 1) ? 1 : 0;
-    return 0;
+    const auto& R = h->res;
+    const bool live = R.running && R.mb && !((volatile PuMailbox*)R.mb)->d.exited;
+    const uint64_t v[10] = {live ? 1u : 0u, R.commands, R.launches, resident_eligible(h, 1) ? 1u : 0u,
+                            R.phase_ticks[0], R.phase_ticks[1], R.phase_ticks[2], R.phase_ticks[3], R.call_ns, 0};
+    for (size_t k = 0; k < n && k < 10; k++) out[k] = v[k];
+    return (int)(n < 9 ? n : 9);
 }
 
 int pu_compiled_config(const pu_handle* h) { return h && h->jit.ok ? (h->jit_throughput ? 2 : 1) : 0; }

@@ -90,7 +90,7 @@ def lib() -> C.CDLL:
         "pu_report": (C.c_long, [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_size_t]),
         "pu_last_kernel_ms": (C.c_double, [C.c_void_p]),
         "pu_set_resident": (C.c_int, [C.c_void_p, C.c_int]),
-        "pu_resident_info": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
+        "pu_resident_info": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_size_t]),
         "pu_last_error": (C.c_char_p, []),
         "pu_version": (C.c_char_p, []),
         "pu_set_replay_mode": (C.c_int, [C.c_void_p, C.c_int]),
@@ -540,11 +540,17 @@ class UncoreManager:
         return rc
 
     def resident_info(self) -> dict:
-        """{running, commands, launches, eligible} of the resident kernel (pu_resident_info)."""
-        out = (C.c_uint64 * 4)()
-        if lib().pu_resident_info(self._handle(), out) != 0:
+        """The resident kernel (pu_resident_info): running, commands served,
+        kernels launched, eligible, and per command the mean kernel-side phases
+        (request copy, message loop, close, mailbox) and host-side call time in µs."""
+        out = (C.c_uint64 * 9)()
+        if lib().pu_resident_info(self._handle(), out, 9) < 0:
             raise UncoreError(last_error())
-        return {"running": bool(out[0]), "commands": int(out[1]), "launches": int(out[2]), "eligible": bool(out[3])}
+        n = max(1, int(out[1]))
+        sums_us = {"request_copy": out[4] / 100, "message_loop": out[5] / 100, "close": out[6] / 100,
+                   "mailbox": out[7] / 100, "host_call": out[8] / 1000}
+        return {"running": bool(out[0]), "commands": int(out[1]), "launches": int(out[2]), "eligible": bool(out[3]),
+                "sums_us": sums_us, "mean_us": {k: v / n for k, v in sums_us.items()}}
 
     def stats(self, replica: int = 0) -> A.Stats:
         s = A.Stats()

@@ -19,7 +19,7 @@ git -C "$ROOT" worktree add -f --detach "$WT" "$REF" > /dev/null
 trap 'git -C "$ROOT" worktree remove --force "$WT"' EXIT
 make -C "$WT/primesim_amd/csrc" -j8 ../libprimeuncore.so > "$WT/build.log" 2>&1 || { tail -20 "$WT/build.log"; exit 1; }
 cp "$WT/primesim_amd/libprimeuncore.so" "$ROOT/primesim_amd/libprimeuncore_$NAME.so"
-PRIMEUNCORE_LIB="$ROOT/primesim_amd/libprimeuncore_$NAME.so" python3 - "$ROOT" <<'EOF'
+PRIMEUNCORE_JIT_OFFLINE=1 PRIMEUNCORE_LIB="$ROOT/primesim_amd/libprimeuncore_$NAME.so" python3 - "$ROOT" <<'EOF'
 import ctypes as C, sys
 sys.path.insert(0, sys.argv[1])
 import primesim_amd as P

@@ -1,5 +1,5 @@
 """Register, spill and LDS use of the compiled-configuration kernels of one
-preset: the code object jit.cpp's hipRTC compile produces (pu_config_jit_warm
+preset: the code objects the build-time warm-up (hipcc) produces (pu_config_jit_warm
 into a scratch cache), read from its AMDGPU metadata.  No GPU.
 
     python tools/kernel_resources.py [C4] [--lib primesim_amd/libprimeuncore_X.so]
@@ -22,7 +22,7 @@ KEYS = (".vgpr_count", ".agpr_count", ".sgpr_count", ".vgpr_spill_count", ".sgpr
 
 def resources(preset: str, lib: str | None = None) -> dict:
     with tempfile.TemporaryDirectory() as d:
-        env = dict(os.environ, PRIMEUNCORE_JIT_CACHE=d)
+        env = dict(os.environ, PRIMEUNCORE_JIT_CACHE=d, PRIMEUNCORE_JIT_OFFLINE="1")   # hipcc, as shipped
         if lib:
             env["PRIMEUNCORE_LIB"] = os.path.abspath(lib)
         code = ("import ctypes as C, sys; sys.path.insert(0, %r); import primesim_amd as P; "

@@ -42,7 +42,18 @@ def main() -> None:
             um.allocCore(prog, th)
         um.set_resident(mode)
         um.access_batch(reqs[:100_000])                # warm caches and link histories (one launch)
+        i0 = um.resident_info()
         r = {"call_overhead_us": call_overhead(um, reqs, a.calls)}
+        i1 = um.resident_info()
+        if i1["commands"] > i0["commands"]:
+            # where a resident call's time goes: kernel-side phases, the rest is the
+            # mailbox round trip (host write -> kernel poll, kernel write -> host poll)
+            nc = i1["commands"] - i0["commands"]
+            r["call_overhead_breakdown_us"] = {k: (i1["sums_us"][k] - i0["sums_us"][k]) / nc for k in i1["sums_us"]}
+        t = time.perf_counter()
+        for _ in range(a.calls):
+            P.uncore.lib().pu_num_replicas(um._handle())
+        r["python_ctypes_call_us"] = (time.perf_counter() - t) / a.calls * 1e6
         r.update(measure(um, reqs, a, 100_000))
         r["resident_info"] = um.resident_info()
         out["resident" if mode else "launch_per_call"] = r
