@@ -35,6 +35,7 @@
 #   ab_single:V1,V2,...  the same, one simulation alone only
 #   ab_ens:V1,V2,...     the same, headline only (3 rounds)
 #   ab_c3:V1,V2,...      the same on bench --config C3 (2 rounds)
+#   ab_ensc:V1,V2,...    headline open loop and the same workload closed loop (2 rounds)
 #   ab_driver:V1,V2,...  the headline on the driver's window (--steps 20 --warmup 5), 2 interleaved rounds
 #   refwrap      tools/ref_overhead.py: the reference CPU uncore with and without the golden counting wraps
 #   residency    tools/probe/residency: one-wave workgroups resident per CU by resource shape
@@ -64,6 +65,7 @@ ab() {   # ab ROUNDS MODES VARIANTS
       case $mode in
         ens) ARGS="--steps 5 --warmup 5 --no-cpu --no-extras";;
         c3) ARGS="--config C3 --steps 5 --warmup 5 --no-cpu --no-extras";;
+        ensc) ARGS="--steps 5 --warmup 5 --no-cpu --no-extras --replay closed";;
         c5) ARGS="--config C5 --steps 5 --warmup 5 --no-cpu --no-extras";;
         single) ARGS="--replicas 1 --steps 3 --warmup 5 --no-cpu --no-extras";;
         closed) ARGS="--replicas 1 --steps 3 --warmup 5 --no-cpu --no-extras --replay closed";;
@@ -118,6 +120,7 @@ for S in "$@"; do
     ab_single:*) ab 2 "single closed" "${S#ab_single:}" > ${O}_ab_single.txt || exit 1;;
     ab_ens:*) ab 3 "ens" "${S#ab_ens:}" > ${O}_ab_ens.txt || exit 1;;
     ab_c3:*) ab 2 "c3" "${S#ab_c3:}" > ${O}_ab_c3.txt || exit 1;;
+    ab_ensc:*) ab 2 "ens ensc" "${S#ab_ensc:}" > ${O}_ab_ensc.txt || exit 1;;
     ab_driver:*) for i in 1 2; do for v in $(echo "${S#ab_driver:}" | tr ',' ' '); do
                ( variant_env "$v"
                  timeout -k 10 400 $BENCH $DRIVER --no-cpu --no-extras 2>>${O}_ab.err | python -c "import json,sys; b=json.loads(sys.stdin.read().strip().splitlines()[-1]); c=b['config']; p=c.get('replica_pool') or {}; print('driver', '$v', round(b['value']/1e6,2), 'M/s', 'replicas', c['replicas_per_gpu'], 'slots', c['wavefronts_per_gpu'], 'halted', c['halted_replicas'], 'busy', round(p.get('busy_fraction', 0), 4), 'started', p.get('replicas_started'), flush=True)" >> ${O}_ab_driver.txt ) || exit 1
