@@ -2547,9 +2547,13 @@ __device__ __forceinline__ pu_req req_unpack16(v2u64 w) {
 // request not processed goes to *pos_out (if given); returns whether the
 // range is done.
 template <int NL, bool SLICED, bool LH>
-__device__ __forceinline__ bool replica_loop(Engine<NL, LH>& e, const pu_req* __restrict__ reqs,
-                                             int32_t* __restrict__ delays, uint64_t b, uint64_t end,
-                                             uint64_t* __restrict__ pos_out, uint64_t deadline, uint32_t flags) {
+__device__ __forceinline__ bool replica_steps(Engine<NL, LH>& e, const pu_req* __restrict__ reqs,
+                                              int32_t* __restrict__ delays, uint64_t b, uint64_t end,
+                                              uint64_t* __restrict__ pos_out);
+// The message loop's state from the replica's RunState (lane 0 into lds_ctl,
+// lds_eng), counters zeroed: the start of a launch's work on one replica.
+template <int NL, bool LH>
+__device__ __forceinline__ void replica_begin(Engine<NL, LH>& e, uint64_t deadline, uint32_t flags) {
     e.hq_head = 0;
     stats_init();
     e.dly = 0;
@@ -2575,6 +2579,22 @@ __device__ __forceinline__ bool replica_loop(Engine<NL, LH>& e, const pu_req* __
     __builtin_amdgcn_wave_barrier();
     e.init_shared((int32_t)rl32(e.ln == 0 ? (uint32_t)rs->pool_top : 0u, 0), rl64(e.ln == 0 ? rs->page_next : 0ull, 0),
                   rl64(e.ln == 0 ? rs->last_addr : 0ull, 0));
+}
+
+template <int NL, bool SLICED, bool LH>
+__device__ __forceinline__ bool replica_loop(Engine<NL, LH>& e, const pu_req* __restrict__ reqs,
+                                             int32_t* __restrict__ delays, uint64_t b, uint64_t end,
+                                             uint64_t* __restrict__ pos_out, uint64_t deadline, uint32_t flags) {
+    replica_begin<NL, LH>(e, deadline, flags);
+    return replica_steps<NL, SLICED, LH>(e, reqs, delays, b, end, pos_out);
+}
+
+// The requests [b, end) through prime.cpp's message loop on the state in
+// lds_ctl / lds_eng (replica_begin).
+template <int NL, bool SLICED, bool LH>
+__device__ __forceinline__ bool replica_steps(Engine<NL, LH>& e, const pu_req* __restrict__ reqs,
+                                              int32_t* __restrict__ delays, uint64_t b, uint64_t end,
+                                              uint64_t* __restrict__ pos_out) {
     uint64_t i = b;
     for (; i < end; i++) {
         if (SLICED && __builtin_amdgcn_s_memrealtime() >= uni64(lds_ctl.deadline)) break;
@@ -2715,21 +2735,26 @@ __device__ __forceinline__ bool replica_run(Engine<NL, LH>& e, char* __restrict_
 // Resident mode (MODE 3, latency kernels only; geometry.h PuMailbox): one
 // two-wave workgroup stays on the GPU for replica `rep` and serves the host's
 // commands — a lone uncore_access (uncore_manager.cpp:82-85, prime.cpp:129)
-// or a short host batch — without a launch per call, with the replica's
-// queue headers kept in the CU's LDS image across calls (the ~17 µs image copy
-// of a latency launch is paid once).  Each command is exactly one launch's
-// work: replica_loop over the requests (copied from the host's mailbox into
-// device memory first) and replica_close (run state and counters back to
-// HBM), so results are those of the launch path.  Delays go straight into the
-// host buffer; `ack` is published after a system-scope release, so the host
-// sees every delay, every counter and the run state when it sees the ack.
-// The kernel leaves on a STOP command or after `idle_ticks` (s_memrealtime,
-// 100 MHz) without one: a persistent kernel that always drains by itself.
+// or a short host batch — without a launch per call.  Across commands it
+// keeps in its CU what a launch would reload and write back: the queue-header
+// image (LDS), the message loop's run state (lds_ctl / lds_eng) and the
+// counter sums (lds_stat, lds_err), which go back to HBM (replica_close) once,
+// when the kernel leaves; the host stops it before anything reads them
+// (uncore.cpp resident_quiesce).  Each command runs replica_steps over its
+// requests with exactly the per-launch transitions of replica_begin /
+// replica_close (the halted flag under PU_KF_NOHALT, the engine-limit stop,
+// the first limit position), so results are the launch path's.  A one-request
+// command travels inside the command line itself; longer ones are copied from
+// the mailbox's request area into device memory.  Delays go straight into the
+// host buffer; `ack` follows a system-scope release.  The kernel leaves on a
+// STOP command or after `idle_ticks` (s_memrealtime, 100 MHz) without one: a
+// persistent kernel that always drains by itself.
 struct ResCtl {
     uint64_t seq;      // the last command taken
     uint64_t n;        // its requests
-    uint64_t err;      // the replica's error flags (EngineStats.error_flags)
+    uint64_t err;      // the replica's error flags in HBM when the kernel started
     uint32_t flags, cmd;
+    int32_t halted;    // RunState.halted between commands
 };
 static __shared__ ResCtl lds_res;
 
@@ -2751,15 +2776,23 @@ __device__ __forceinline__ void resident_body(const Geo* __restrict__ g, char* _
     e.base = arena + (size_t)rep * OFF(g->replica_bytes);
     char* hb = e.base + OFF(g->off_qhdr);
     const uint32_t nq = (uint32_t)g->nqueues;
+    const AS1 v4u32* hline = (const AS1 v4u32*)(AS1 char*)(char*)&mb->h;
     const AS1 v4u32* hreq = (const AS1 v4u32*)(AS1 char*)(char*)(mb + 1);
     int32_t* hdelay = reinterpret_cast<int32_t*>(reinterpret_cast<pu_req*>(mb + 1) + cap);
+    AS1 v4u32* dst = (AS1 v4u32*)(AS1 char*)(char*)stage;
     hdr_image_in(hb, nq, threadIdx.x);        // threads 0..127: pieces t, t + 128, ...
-    if (!helper && e.ln == 0) {
-        lds_res.seq = sys_load_u64(&mb->d.ack);   // the host sets ack = seq before the launch
-        lds_res.err = e.template at<EngineStats>(OFF(g->off_stats))->error_flags;
+    if (helper) {
+        __syncthreads();                      // [S] replica_begin's stats_init
+    } else {
+        replica_begin<NL, LH>(e, UINT64_MAX, 0u);   // run state and counters, once per kernel   [S]
+        if (e.ln == 0) {
+            lds_res.seq = sys_load_u64(&mb->d.ack);   // the host sets ack = seq before the launch
+            lds_res.err = e.template at<EngineStats>(OFF(g->off_stats))->error_flags;
+            lds_res.halted = lds_ctl.halted0;
+        }
     }
-    __syncthreads();
     for (;;) {
+        uint64_t tk0 = 0;
         if (!helper) {
             // lane 0 polls the host's command word; the other lanes wait with it
             const uint64_t last = uni64(lds_res.seq);
@@ -2771,33 +2804,35 @@ __device__ __forceinline__ void resident_body(const Geo* __restrict__ g, char* _
                 if (sq != last || __builtin_amdgcn_s_memrealtime() >= t_idle) break;
                 __builtin_amdgcn_s_sleep(2);
             }
-            if (sq != last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // the command's fields and requests
-            if (e.ln == 0) {
-                if (sq != last) {
-                    const volatile PuResHost* H = &mb->h;
-                    lds_res.n = H->n;
-                    lds_res.flags = H->flags;
-                    lds_res.cmd = H->cmd;
+            tk0 = __builtin_amdgcn_s_memrealtime();
+            if (sq != last) {
+                // the whole command line in one round trip (written before seq):
+                // lane 0 {seq, n | flags | cmd}, lanes 1-2 the inline request
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                v4u32 w = v4u32{0u, 0u, 0u, 0u};
+                if (e.ln < 3) w = *(const volatile AS1 v4u32*)&hline[e.ln];
+                const uint32_t n = rl32(w.z, 0), fc = rl32(w.w, 0);
+                if (fc >> 16 == PU_RES_RUN && n == 1 && (e.ln == 1 || e.ln == 2)) dst[e.ln - 1] = w;
+                if (e.ln == 0) {
+                    lds_res.n = n;
+                    lds_res.flags = fc & 0xFFFFu;
+                    lds_res.cmd = fc >> 16;
                     lds_res.seq = sq;
-                } else {
-                    lds_res.cmd = PU_RES_STOP;        // idle: leave
                 }
+            } else if (e.ln == 0) {
+                lds_res.cmd = PU_RES_STOP;            // idle: leave
             }
         }
         __syncthreads();                              // [A] the command is in LDS
         if (uni32(lds_res.cmd) != PU_RES_RUN) break;
         const uint64_t n = min(uni64(lds_res.n), cap);
         if (helper) {
-            __syncthreads();                          // [B] replica_loop's stats_init
+            __syncthreads();                          // [B] the command's state is set
             mg1_helper(g, e.base, stage, 0, n);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no prefetch DMA outlives the command
-            __syncthreads();                          // [C] the main wave left its loop
-            __syncthreads();                          // [D] replica_close
-            continue;
+            continue;                                 // to [A]: the main wave has left its loop
         }
-        const uint64_t tk0 = __builtin_amdgcn_s_memrealtime();
-        {   // the requests: host mailbox -> device staging, 16 B per lane and step, 4 steps in flight
-            AS1 v4u32* dst = (AS1 v4u32*)(AS1 char*)(char*)stage;
+        if (n > 1) {   // the requests: mailbox -> device staging, 16 B per lane and step, 4 steps in flight
             const uint64_t pieces = 2 * n;
             for (uint64_t k = (uint64_t)e.ln; k < pieces; k += 256) {
                 v4u32 a0 = v4u32{0u, 0u, 0u, 0u}, a1 = a0, a2 = a0, a3 = a0;
@@ -2810,36 +2845,56 @@ __device__ __forceinline__ void resident_body(const Geo* __restrict__ g, char* _
                 if (k + 128 < pieces) dst[k + 128] = a2;
                 if (k + 192 < pieces) dst[k + 192] = a3;
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint64_t tk1 = __builtin_amdgcn_s_memrealtime();
+        // replica_begin's per-launch transitions, on the state kept in LDS
+        const uint32_t fl = uni32(lds_res.flags);
         if (e.ln == 0) {
+            const int32_t h0 = lds_res.halted;
+            lds_ctl.halted0 = h0;
+            lds_ctl.halted = (fl & PU_KF_NOHALT) ? 0 : h0;
+            lds_ctl.flags = fl;
+            lds_ctl.cur = 0;
+            lds_ctl.limit_at = UINT64_MAX;
+            lds_eng.stop = 0;
             lds_hq_head = 0;
             lds_main_done = 0;
         }
-        const uint64_t tk1 = __builtin_amdgcn_s_memrealtime();
-        replica_loop<NL, false, LH>(e, stage, hdelay, 0, n, nullptr, UINT64_MAX, uni32(lds_res.flags));   // [B]
-        if (e.ln == 0) *(volatile AS3 uint32_t*)&lds_main_done = 1u;
+        e.dly = 0;
+        e.hit = false;
+        e.hq_head = 0;
+        __syncthreads();                              // [B]
+        replica_steps<NL, false, LH>(e, stage, hdelay, 0, n, nullptr);
         const uint64_t tk2 = __builtin_amdgcn_s_memrealtime();
-        __syncthreads();                              // [C]
-        replica_close<NL, LH>(e);                     // [D]
-        const uint64_t tk3 = __builtin_amdgcn_s_memrealtime();
         if (e.ln == 0) {
-            lds_res.err |= lds_err;
+            *(volatile AS3 uint32_t*)&lds_main_done = 1u;
+            // replica_close's halted rule
+            lds_res.halted = (fl & PU_KF_NOHALT) ? (lds_ctl.halted0 | lds_ctl.halted) : lds_ctl.halted;
             volatile PuResDev* Dv = &mb->d;
-            Dv->err = lds_res.err;
+            Dv->err = lds_res.err | lds_err;
             Dv->last_addr = lds_eng.last_addr;
             Dv->phase[0] = (uint32_t)(tk1 - tk0);
             Dv->phase[1] = (uint32_t)(tk2 - tk1);
-            Dv->phase[2] = (uint32_t)(tk3 - tk2);
-            Dv->phase[3] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tk3);
+            Dv->phase[2] = 0u;
+            Dv->phase[3] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - tk2);
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: delays, counters, run state visible
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the delays and the mailbox visible
         if (e.ln == 0) __hip_atomic_store(&mb->d.ack, uni64(lds_res.seq), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    hdr_image_out(hb, nq, threadIdx.x);              // the headers back to HBM
-    __syncthreads();
+    // leave: the headers, the run state and the counters back to HBM
+    hdr_image_out(hb, nq, threadIdx.x);
+    if (helper) {
+        __syncthreads();                              // replica_close's barrier
+        return;
+    }
+    if (e.ln == 0) {
+        lds_ctl.flags = 0u;                           // replica_close writes lds_ctl.halted as the run state's
+        lds_ctl.halted = lds_res.halted;
+    }
+    replica_close<NL, LH>(e);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    if (!helper && e.ln == 0) __hip_atomic_store(&mb->d.exited, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (e.ln == 0) __hip_atomic_store(&mb->d.exited, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // One workgroup (= one wavefront) per replica.  Replica replica0 + blockIdx.x

@@ -34,6 +34,7 @@
 // read-after-write is a same-thread program-order dependency.
 #pragma once
 
+#include <stddef.h>
 #include <stdint.h>
 
 #define PU_QRING 128          // ring capacity (history tree holds <= 100 intervals)
@@ -219,12 +220,12 @@ struct Geo {
 // STOP command or after `idle` ticks without one.
 #define PU_RES_RUN 0u
 #define PU_RES_STOP 1u
-struct PuResHost {          // written by the host (its own 64-B line)
+struct PuResHost {          // written by the host (its own 64-B line), seq last
     uint64_t seq;           // command number: the kernel waits for a change
-    uint64_t n;             // requests of the command (in PuMailbox's request area)
-    uint32_t flags;         // PU_KF_* of the command
-    uint32_t cmd;           // PU_RES_RUN / PU_RES_STOP
-    uint64_t _pad[5];
+    uint32_t n;             // requests of the command (n > 1: in PuMailbox's request area)
+    uint32_t flags_cmd;     // PU_KF_* of the command | (PU_RES_RUN / PU_RES_STOP) << 16
+    uint64_t req0[4];       // n == 1: the request itself (a pu_req, 32 B at offset 16)
+    uint64_t _pad[2];
 };
 struct PuResDev {           // written by the kernel (its own 64-B line)
     uint64_t ack;           // seq of the last command completed
@@ -235,6 +236,8 @@ struct PuResDev {           // written by the kernel (its own 64-B line)
                             // replica_loop, replica_close, mailbox writes up to the ack
     uint64_t _pad[2];
 };
+static_assert(sizeof(PuResHost) == 64 && sizeof(PuResDev) == 64, "one 64-B line each");
+static_assert(offsetof(PuResHost, req0) == 16, "the inline request is lanes 1-2 of the line's 16-B pieces");
 // Mailbox: {host line, device line}, then pu_req reqs[cap], then int32 delays[cap].
 struct PuMailbox {
     PuResHost h;

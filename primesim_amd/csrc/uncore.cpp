@@ -436,7 +436,7 @@ int resident_stop(pu_handle* h) {
     if (!R.running) return 0;
     volatile PuMailbox* mb = R.mb;
     if (!mb->d.exited) {
-        mb->h.cmd = PU_RES_STOP;
+        mb->h.flags_cmd = PU_RES_STOP << 16;
         mb->h.n = 0;
         std::atomic_thread_fence(std::memory_order_release);
         mb->h.seq = ++R.seq;
@@ -458,7 +458,7 @@ void resident_atexit() {
         auto& R = h->res;
         if (!R.running || !R.mb) continue;
         volatile PuMailbox* mb = R.mb;
-        mb->h.cmd = PU_RES_STOP;
+        mb->h.flags_cmd = PU_RES_STOP << 16;
         std::atomic_thread_fence(std::memory_order_release);
         mb->h.seq = ++R.seq;
         const auto t0 = std::chrono::steady_clock::now();
@@ -515,10 +515,11 @@ int resident_run(pu_handle* h, int replica, const pu_req* reqs, size_t n, uint32
     if (rc) return rc;
     volatile PuMailbox* mb = R.mb;
     const auto t0 = std::chrono::steady_clock::now();
-    std::memcpy(R.mb + 1, reqs, n * sizeof(pu_req));
-    mb->h.n = n;
-    mb->h.flags = flags;
-    mb->h.cmd = PU_RES_RUN;
+    static_assert(sizeof(pu_req) == sizeof(PuResHost::req0), "a request fits the command line");
+    if (n == 1) std::memcpy((void*)mb->h.req0, reqs, sizeof(pu_req));   // travels with the command
+    else std::memcpy(R.mb + 1, reqs, n * sizeof(pu_req));
+    mb->h.n = (uint32_t)n;
+    mb->h.flags_cmd = (flags & 0xFFFFu) | (PU_RES_RUN << 16);
     std::atomic_thread_fence(std::memory_order_release);
     const uint64_t seq = ++R.seq;
     mb->h.seq = seq;
