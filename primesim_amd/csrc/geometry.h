@@ -237,7 +237,7 @@ struct PuResDev {           // written by the kernel (its own 64-B line)
     uint64_t _pad[2];
 };
 static_assert(sizeof(PuResHost) == 64 && sizeof(PuResDev) == 64, "one 64-B line each");
-static_assert(offsetof(PuResHost, req0) == 16, "the inline request is lanes 1-2 of the line's 16-B pieces");
+static_assert(__builtin_offsetof(PuResHost, req0) == 16, "the inline request is lanes 1-2 of the line's 16-B pieces");
 // Mailbox: {host line, device line}, then pu_req reqs[cap], then int32 delays[cap].
 struct PuMailbox {
     PuResHost h;
