@@ -195,10 +195,17 @@ constexpr int ring_pf() { return LH ? PU_RING_PF : PU_RING_PF_TP; }
 #define PU_WAVES_1LEVEL 5
 #endif
 #endif
-// Deeper hierarchies (NL > 1): the compiler's choice unless PU_WAVES_DEEP is
-// set (tools/gpu_session.sh V@-DPU_WAVES_DEEP=W A/Bs of bench --config C3).
+// Deeper hierarchies (NL > 1), compiled configuration: 4 waves per SIMD (128
+// VGPRs, no spill at C3, where the compiler's own choice was 150 VGPRs = 3
+// waves): C3 +20% (448.1 / 449.4 vs 373.4 / 373.2 M/s; 5 waves, 31 VGPRs
+// spilled, +13%; profiles/r6e_ab_c3.txt, same box).  The ahead-of-time
+// kernels keep the compiler's choice.
 #ifndef PU_WAVES_DEEP
+#if defined(PU_JIT_GEO)
+#define PU_WAVES_DEEP 4
+#else
 #define PU_WAVES_DEEP 1
+#endif
 #endif
 #define PU_MIN_WAVES(NL) ((NL) == 1 ? PU_WAVES_1LEVEL : PU_WAVES_DEEP)
 // native vectors (not classes), so loads/stores through global-address-space
@@ -417,9 +424,14 @@ __device__ __forceinline__ void ring_load(const NetCtx& c, int q, uint32_t head,
 // (counts, cycle sums and their ratios), where those steps are the identity,
 // so the result is the same correctly rounded quotient.  The refined
 // reciprocal of a shared divisor is computed once.
+// PU_DIV_NR1: one Newton step instead of two before the residual correction
+// (an A/B knob; tools/probe/rcp_probe.hip measures whether gfx950's v_rcp_f64
+// is accurate enough for it to stay correctly rounded).
 __device__ __forceinline__ double rcp_nr(double b) {
     double y = __builtin_amdgcn_rcp(b);
+#ifndef PU_DIV_NR1
     y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+#endif
     return __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
 }
 __device__ __forceinline__ double div_nr(double a, double b, double y) {

@@ -18,6 +18,7 @@
 #   sq_closed / traffic_closed / regions_closed  the headline kernel's SQ counters, fabric traffic and region
 #                profile on the closed-loop replay of the same workload (bench --replay closed)
 #   sq_single    the same for one simulation alone, open loop and closed loop (latency kernel)
+#   rcp          tools/probe/rcp_probe: v_rcp_f64 accuracy and one- vs two-step correctly rounded division
 #   handoff      tools/probe/handoff: dependent hand-off latency between two waves
 #   tworank      bench.py --gpus 2 with both ranks on card 0 (gloo)
 #   sweep        tools/relax/sweep_bench: one relaxation sweep's phases L and F on the GPU, W = 1,024 and 4,096
@@ -99,6 +100,7 @@ for S in "$@"; do
     regions_closed) timeout -k 10 300 python tools/prof_regions.py --jit -- --steps 3 --warmup 5 --no-cpu --no-extras --replay closed > ${O}_regions_closed.txt 2>&1 || exit 1;;
     sq_single) timeout -k 10 500 python tools/pmc_sq.py --kernel pu_jit_uncore_s1_h1 --work /tmp/pmc_sq1 --out ${O}_sq_single_open.json -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras > ${O}_sq_single_open.log 2>&1 || exit 1
                timeout -k 10 500 python tools/pmc_sq.py --kernel pu_jit_uncore_s1_h1 --work /tmp/pmc_sq2 --out ${O}_sq_single_closed.json -- --replicas 1 --steps 2 --warmup 5 --no-cpu --no-extras --replay closed > ${O}_sq_single_closed.log 2>&1 || exit 1;;
+    rcp) timeout -k 10 120 tools/probe/rcp_probe 4096 > ${O}_rcp.json 2> ${O}_rcp.log || exit 1;;
     handoff) timeout -k 10 120 tools/probe/handoff > ${O}_handoff.json 2> ${O}_handoff.log || exit 1;;
     tworank) PU_BENCH_DEVICE=0 timeout -k 10 300 $BENCH --gpus 2 --steps 3 --warmup 2 --no-cpu --dist-backend gloo > ${O}_two_rank.json 2> ${O}_two_rank.log || exit 1;;
     tworank_parity) PU_BENCH_DEVICE=0 timeout -k 10 400 $BENCH --gpus 2 --steps 3 --warmup 2 --dist-backend gloo > ${O}_two_rank_parity.json 2> ${O}_two_rank_parity.log || exit 1;;
