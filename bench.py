@@ -78,9 +78,10 @@ METRIC = "simulated memory accesses/sec (uncore) at 1024 cores; % HBM roofline"
 # configuration (BASELINE.json configs[3]); C3 and C5 are the deeper and the
 # larger shapes, measured the same way (their lines name their own metric).
 WORKLOADS = {
-    # (C3's replicas run ~2x faster than C4's: twice the chunk, so the timed
-    # window outlasts the 20 slices and the pool never runs dry)
-    "C3": {"cores": 256, "stream": "PU_STREAM_MULTIPROGRAM", "num_progs": 4, "replay": "open", "chunk": 81920,
+    # (C3's replicas run ~2x faster than C4's: 1.5x the chunk, so the timed
+    # window outlasts the 20 slices for most replicas and HBM still holds ~10%
+    # spare replicas for the pool; at 2x only 8 spares fit: busy 0.93)
+    "C3": {"cores": 256, "stream": "PU_STREAM_MULTIPROGRAM", "num_progs": 4, "replay": "open", "chunk": 61440,
            "desc": "C3: 256-core 16x16 mesh, private L1 32KB/8W + private L2 256KB/8W/5cyc + 1MB/16W shared-LLC "
                    "slice per tile, directory MESI full-map; multi-programmed mix, 4 programs x 64 cores, "
                    "per-program footprints 4-64 MB, 20% writes"},
@@ -651,7 +652,7 @@ def parse_args(argv=None):
     ap.add_argument("--spare-replicas", type=float, default=0.1,
                     help="replicas beyond the resident wavefront slots, as a fraction of them (replica pool)")
     ap.add_argument("--chunk", type=int, default=0,
-                    help="requests per replica per step (0 = the configuration's: 40,960 for C4 and C5, 81,920 for C3)")
+                    help="requests per replica per step (0 = the configuration's: 40,960 for C4 and C5, 61,440 for C3)")
     ap.add_argument("--slice-ms", type=float, default=400.0,
                     help="timed steps are wall-time slices: every replica continues its own stream for this long "
                          "per launch (stopping only between requests); 0 = fixed --chunk requests per replica per step")
