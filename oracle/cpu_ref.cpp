@@ -41,6 +41,7 @@
 #ifdef CPUREF_TRACE
 void cpuref_trace_link(size_t link, bool tree, size_t intervals);   // defined by the analysis build
 static size_t g_trace_k;   // index (from the front) of the interval the last tree search stopped at
+static size_t g_trace_n0, g_trace_n1;   // free intervals before the last queue op (after the prune) and after it
 #endif
 
 namespace {
@@ -75,6 +76,9 @@ uint64_t mg1_wait(const Queue& q) {
 uint64_t queue_delay(Queue& q, uint64_t t, uint64_t p, uint64_t min_proc, uint64_t* mg1_calls) {
     auto& v = q.iv;
     if (v.size() >= 100) v.erase(v.begin());          // prune the minimum
+#ifdef CPUREF_TRACE
+    g_trace_n0 = v.size();
+#endif
     uint64_t d;
     if (v.front().first > t + p) {                     // older than tracked history: M/G/1
         d = mg1_wait(q);
@@ -118,6 +122,9 @@ uint64_t queue_delay(Queue& q, uint64_t t, uint64_t p, uint64_t min_proc, uint64
     q.n++;
     uint64_t fin = t + d + p;
     if (fin > q.newest) q.newest = fin;
+#ifdef CPUREF_TRACE
+    g_trace_n1 = v.size();
+#endif
     return d;
 }
 
