@@ -89,3 +89,13 @@ def test_gpus_must_match_world_size(tmp_path):
              {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2
     assert "refusing" in r.stderr
+
+
+def test_other_configurations_keep_the_contract(tmp_path):
+    """--config C3: the same line for the 256-core three-level shape (its own
+    stream and metric), with the per-rank reference parity."""
+    r = _run([*PARITY_ARGS, "--config", "C3"], tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    b = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert "256 cores (C3)" in b["metric"] and b["config"]["workload"].startswith("C3:")
+    assert b["parity"] is True and len(b["rank_parity"]["per_rank"]) == 2
