@@ -379,8 +379,11 @@ int pu_access_batch(pu_handle* h, int replica, const pu_req* reqs, size_t n,
  * kernel), -1 query; returns the previous mode.  pu_resident_info writes up
  * to n of {kernel running, commands served, kernels launched, eligible, then
  * summed over the commands: the kernel's request-copy, message-loop, close
- * (run state and counters) and mailbox phases in 10-ns ticks, and the host's
- * post-to-answer time in ns} and returns how many it wrote. */
+ * (run state and counters) and mailbox phases in 10-ns ticks (commands with a
+ * full answer), the host's post-to-answer time in ns, and how many commands
+ * came back as the fast answer (one request, no new error bit, no TLB: the
+ * delay and the command number in one 8-B store)} and returns how many it
+ * wrote. */
 int pu_set_resident(pu_handle* h, int mode);
 int pu_resident_info(pu_handle* h, uint64_t* out, size_t n);
 

@@ -265,7 +265,8 @@ struct LoopCtl {
     uint64_t done;         // requests processed in this launch
     int32_t D;             // prime.cpp's running `delay` of the open message
     int32_t halted, halted0, skip;
-    uint32_t flags, _pad;
+    uint32_t flags;
+    int32_t last_d;        // latency kernels: the last request's delay (0: none ran), for the resident fast answer
     uint64_t cur;          // index of the request being simulated
     uint64_t limit_at;     // first request that raised a PU_ERRF_LIMITS bit (UINT64_MAX: none)
 };
@@ -2624,7 +2625,10 @@ __device__ __forceinline__ bool replica_steps(Engine<NL, LH>& e, const pu_req* _
         }
         __builtin_amdgcn_wave_barrier();
         if (uni32((uint32_t)lds_ctl.skip)) {     // PU_KF_MSGHALT: this message's receive thread has exited
-            if (e.ln == 0) delays[i] = 0;
+            if (e.ln == 0) {
+                delays[i] = 0;
+                if constexpr (LH) lds_ctl.last_d = 0;
+            }
             continue;
         }
         PROF_ADD(PF_REQ, p_loop);
@@ -2637,6 +2641,7 @@ __device__ __forceinline__ bool replica_steps(Engine<NL, LH>& e, const pu_req* _
             lds_ctl.D = D;
             lds_ctl.done++;
             delays[i] = d;
+            if constexpr (LH) lds_ctl.last_d = d;
             if (core_ok) {
                 e.template at<int64_t>(OFF(e.g->off_completion))[q.core] = t + d;
                 if (lds_ctl.flags & PU_KF_CLOSED)
@@ -2869,10 +2874,12 @@ __device__ __forceinline__ void resident_body(const Geo* __restrict__ g, char* _
             lds_ctl.flags = fl;
             lds_ctl.cur = 0;
             lds_ctl.limit_at = UINT64_MAX;
+            lds_ctl.last_d = 0;
             lds_eng.stop = 0;
             lds_hq_head = 0;
             lds_main_done = 0;
         }
+        const uint64_t err0 = uni64(lds_err);
         e.dly = 0;
         e.hit = false;
         e.hq_head = 0;
@@ -2883,6 +2890,20 @@ __device__ __forceinline__ void resident_body(const Geo* __restrict__ g, char* _
             *(volatile AS3 uint32_t*)&lds_main_done = 1u;
             // replica_close's halted rule
             lds_res.halted = (fl & PU_KF_NOHALT) ? (lds_ctl.halted0 | lds_ctl.halted) : lds_ctl.halted;
+        }
+        // The fast answer: a one-request command that raised no error bit, on a
+        // configuration without TLB translation, needs nothing but its delay,
+        // which travels with the command's seq in one 8-B store (atomic to the
+        // host; the host already holds the error flags): no release fence, no
+        // other mailbox store.  Everything else takes the full answer below.
+        if (n == 1 && uni64(lds_err) == err0 && !g->tlb_enable) {
+            if (e.ln == 0)
+                __hip_atomic_store(&mb->d.fast, (uint64_t)(uint32_t)uni64(lds_res.seq) |
+                                                    ((uint64_t)(uint32_t)lds_ctl.last_d << 32),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            continue;
+        }
+        if (e.ln == 0) {
             volatile PuResDev* Dv = &mb->d;
             Dv->err = lds_res.err | lds_err;
             Dv->last_addr = lds_eng.last_addr;

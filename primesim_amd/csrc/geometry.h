@@ -234,7 +234,8 @@ struct PuResDev {           // written by the kernel (its own 64-B line)
     uint32_t exited, _pad0; // 1 once the kernel has left (stop or idle)
     uint32_t phase[4];      // the command's phases in s_memrealtime ticks (10 ns): request copy,
                             // replica_loop, replica_close, mailbox writes up to the ack
-    uint64_t _pad[2];
+    uint64_t fast;          // the fast answer of a one-request command: seq (low 32 bits) | delay << 32
+    uint64_t _pad;
 };
 static_assert(sizeof(PuResHost) == 64 && sizeof(PuResDev) == 64, "one 64-B line each");
 static_assert(__builtin_offsetof(PuResHost, req0) == 16, "the inline request is lanes 1-2 of the line's 16-B pieces");

@@ -330,7 +330,9 @@ struct pu_handle {
         hipEvent_t after = nullptr; // orders the kernel after the handle's stream
         uint64_t idle_ticks = 5000000;   // 50 ms of s_memrealtime (100 MHz)
         uint64_t commands = 0, launches = 0;
-        uint64_t phase_ticks[4] = {0, 0, 0, 0};   // summed kernel-side phases (PuResDev.phase)
+        uint64_t phase_ticks[4] = {0, 0, 0, 0};   // summed kernel-side phases (PuResDev.phase, full answers)
+        uint64_t err = 0;                         // the replica's error flags as of the last full answer
+        uint64_t fast = 0;                        // commands answered by the fast word
         uint64_t call_ns = 0;                     // summed host-side post-to-ack time
     } res;
     std::mutex mu;
@@ -443,7 +445,8 @@ int resident_stop(pu_handle* h) {
     }
     R.running = false;
     HIP_TRY(hipStreamSynchronize(R.stream), PU_EIO);
-    R.acked = mb->d.ack;
+    // (commands answered by the fast word leave d.ack behind: R.acked knows them)
+    R.acked = std::max<uint64_t>(R.acked, (uint64_t)mb->d.ack);
     R.seq = R.acked;   // a STOP is never acked; the next kernel starts from the last completed command
     return 0;
 }
@@ -489,6 +492,14 @@ int resident_ensure(pu_handle* h, int replica) {
         if (g_res_handles.empty()) std::atexit(resident_atexit);
         g_res_handles.push_back(h);
     }
+    {   // the error flags this kernel starts from (fast answers do not carry them; full answers do)
+        uint64_t e0 = 0;
+        HIP_TRY(hipMemcpyAsync(&e0, h->arena + (size_t)replica * h->geo.replica_bytes + h->geo.off_stats +
+                                        offsetof(EngineStats, error_flags), 8, hipMemcpyDeviceToHost, h->stream),
+                PU_EIO);
+        HIP_TRY(hipStreamSynchronize(h->stream), PU_EIO);
+        R.err = e0;
+    }
     volatile PuMailbox* mb = R.mb;
     mb->d.exited = 0;
     mb->d.ack = R.acked;   // the kernel waits for seq != ack: a posted, unacked command runs first
@@ -523,14 +534,24 @@ int resident_run(pu_handle* h, int replica, const pu_req* reqs, size_t n, uint32
     std::atomic_thread_fence(std::memory_order_release);
     const uint64_t seq = ++R.seq;
     mb->h.seq = seq;
+    // a one-request command may come back as the fast word {seq, delay}
+    bool fast = false;
     for (uint64_t spin = 1;; spin++) {
+        if (n == 1) {
+            const uint64_t f = mb->d.fast;
+            if ((uint32_t)f == (uint32_t)seq) {
+                fast = true;
+                if (delay_out) delay_out[0] = (int32_t)(uint32_t)(f >> 32);
+                break;
+            }
+        }
         if (mb->d.ack == seq) break;
         if ((spin & 1023) == 0) {
             if (mb->d.exited && mb->d.ack != seq) {
                 // it left (idle) just before the command arrived: a new kernel takes it
                 R.running = false;
                 HIP_TRY(hipStreamSynchronize(R.stream), PU_EIO);
-                R.acked = mb->d.ack;
+                R.acked = std::max<uint64_t>(R.acked, (uint64_t)mb->d.ack);
                 rc = resident_ensure(h, replica);
                 if (rc) return rc;
                 continue;
@@ -544,10 +565,17 @@ int resident_run(pu_handle* h, int replica, const pu_req* reqs, size_t n, uint32
     std::atomic_thread_fence(std::memory_order_acquire);
     R.acked = seq;
     R.commands++;
-    for (int k = 0; k < 4; k++) R.phase_ticks[k] += mb->d.phase[k];
-    if (delay_out) std::memcpy(delay_out, (const int32_t*)((const pu_req*)(R.mb + 1) + kResCap), n * sizeof(int32_t));
-    *err_out = mb->d.err;
-    if (last_addr) *last_addr = mb->d.last_addr;
+    if (fast) {
+        R.fast++;
+        *err_out = R.err;      // no new error bit (else the kernel answers in full)
+    } else {
+        for (int k = 0; k < 4; k++) R.phase_ticks[k] += mb->d.phase[k];
+        if (delay_out)
+            std::memcpy(delay_out, (const int32_t*)((const pu_req*)(R.mb + 1) + kResCap), n * sizeof(int32_t));
+        R.err = mb->d.err;
+        *err_out = R.err;
+        if (last_addr) *last_addr = mb->d.last_addr;
+    }
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     h->last_ms = ms;
     R.call_ns += (uint64_t)(ms * 1e6);
@@ -741,9 +769,10 @@ int pu_resident_info(pu_handle* h, uint64_t* out, size_t n) {
     const auto& R = h->res;
     const bool live = R.running && R.mb && !((volatile PuMailbox*)R.mb)->d.exited;
     const uint64_t v[10] = {live ? 1u : 0u, R.commands, R.launches, resident_eligible(h, 1) ? 1u : 0u,
-                            R.phase_ticks[0], R.phase_ticks[1], R.phase_ticks[2], R.phase_ticks[3], R.call_ns, 0};
+                            R.phase_ticks[0], R.phase_ticks[1], R.phase_ticks[2], R.phase_ticks[3], R.call_ns,
+                            R.fast};
     for (size_t k = 0; k < n && k < 10; k++) out[k] = v[k];
-    return (int)(n < 9 ? n : 9);
+    return (int)(n < 10 ? n : 10);
 }
 
 int pu_compiled_config(const pu_handle* h) { return h && h->jit.ok ? (h->jit_throughput ? 2 : 1) : 0; }

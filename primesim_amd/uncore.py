@@ -543,14 +543,16 @@ class UncoreManager:
         """The resident kernel (pu_resident_info): running, commands served,
         kernels launched, eligible, and per command the mean kernel-side phases
         (request copy, message loop, close, mailbox) and host-side call time in µs."""
-        out = (C.c_uint64 * 9)()
-        if lib().pu_resident_info(self._handle(), out, 9) < 0:
+        out = (C.c_uint64 * 10)()
+        if lib().pu_resident_info(self._handle(), out, 10) < 0:
             raise UncoreError(last_error())
         n = max(1, int(out[1]))
+        nfull = max(1, int(out[1]) - int(out[9]))
         sums_us = {"request_copy": out[4] / 100, "message_loop": out[5] / 100, "close": out[6] / 100,
                    "mailbox": out[7] / 100, "host_call": out[8] / 1000}
         return {"running": bool(out[0]), "commands": int(out[1]), "launches": int(out[2]), "eligible": bool(out[3]),
-                "sums_us": sums_us, "mean_us": {k: v / n for k, v in sums_us.items()}}
+                "fast_answers": int(out[9]), "sums_us": sums_us,
+                "mean_us": {k: v / (n if k == "host_call" else nfull) for k, v in sums_us.items()}}
 
     def stats(self, replica: int = 0) -> A.Stats:
         s = A.Stats()

@@ -49,7 +49,12 @@ def main() -> None:
             # where a resident call's time goes: kernel-side phases, the rest is the
             # mailbox round trip (host write -> kernel poll, kernel write -> host poll)
             nc = i1["commands"] - i0["commands"]
-            r["call_overhead_breakdown_us"] = {k: (i1["sums_us"][k] - i0["sums_us"][k]) / nc for k in i1["sums_us"]}
+            nfast = i1["fast_answers"] - i0["fast_answers"]
+            nfull = nc - nfast
+            r["call_overhead_fast_answers"] = nfast
+            r["call_overhead_breakdown_us"] = {k: (i1["sums_us"][k] - i0["sums_us"][k]) / (nc if k == "host_call" else
+                                                                                          max(1, nfull))
+                                               for k in i1["sums_us"]}
         t = time.perf_counter()
         for _ in range(a.calls):
             P.uncore.lib().pu_num_replicas(um._handle())
