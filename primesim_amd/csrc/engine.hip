@@ -1227,7 +1227,8 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                 vhead = wl32(vhead, head, jt);
                 vcnt = wl32(vcnt, cnt, jt);
                 vf0 = wl64(vf0, f0n, jt);
-                vd = wl64(vd, d, jt);
+                // (hop jt's assumed wait vd is not read again: later M/G/1 finish
+                // times and shifts use the lanes after it)
                 vfin = wl64(vfin, tj + d + (uint64_t)plen, jt);
                 t = tj + d + c.link_delay;
                 js = jt + 1;
