@@ -171,3 +171,38 @@ def test_resident_follows_the_replica_and_can_be_turned_off():
             assert um.stats(r).requests == len(reqs)
     finally:
         um.close()
+
+
+def test_engine_limit_reaches_uncore_access(monkeypatch):
+    """A one-request call is answered by the fast word only when it raised no
+    error bit: with a sharer pool of 2 entries, the uncore_access that runs
+    the pool dry raises (PU_ESTATE through the full answer), and every delay
+    before it is the reference's."""
+    c = Case("c4_allcores")
+    monkeypatch.setenv("PRIMEUNCORE_POOL_ENTRIES", "2")
+    um = P.UncoreManager()
+    um.init(P.load_config(c.xml_path), replicas=1)
+    monkeypatch.delenv("PRIMEUNCORE_POOL_ENTRIES")
+    try:
+        for prog, th in c.threads:
+            um.allocCore(prog, th)
+        D, got, failed_at = 0, [], None
+        for i, q in enumerate(c.reqs):
+            if q["batch_start"]:
+                D = 0
+            try:
+                d = um.uncore_access(int(q["core"]), P.InsMem(int(q["mem_type"]), int(q["prog_id"]), int(q["addr"])),
+                                     int(q["timer"]) + D)
+            except P.UncoreError as e:
+                assert "pool" in str(e)
+                failed_at = i
+                break
+            got.append(d)
+            D = (D + d - 1 + 2**31) % 2**32 - 2**31
+        assert failed_at is not None
+        np.testing.assert_array_equal(np.array(got, np.int32), c.delays[:failed_at])
+        info = um.resident_info()
+        assert info["fast_answers"] >= failed_at - 1 if info["eligible"] else True
+        assert um.error_flags(1)[0] & A.PU_ERRF_POOL
+    finally:
+        um.close()
