@@ -559,6 +559,18 @@ __device__ __forceinline__ uint64_t set_index(uint64_t addr, int offbits, uint64
     return (nsets & (nsets - 1)) == 0 ? (x & (nsets - 1)) : x % nsets;
 }
 
+// LDS staging ring for predicted tree hops: ring_pf<LH>() full link rings per wave
+// (one wave per workgroup), filled by global_load_lds_dwordx4 and consumed in
+// hop order behind a counted vmcnt (loads, stores and LDS-DMA retire in issue
+// order, MI355X_MICROARCH.md §waitcnt; hipcc would drain everything instead).
+static __shared__ v2u64 lds_ring[PU_RING_PF][PU_QRING];        // latency kernel (LH)
+static __shared__ v2u64 lds_ring_tp[PU_RING_PF_TP][PU_QRING];  // throughput kernels
+template <bool LH>
+__device__ __forceinline__ v2u64* ring_slot(int slot) {
+    if constexpr (LH) return lds_ring[slot];
+    else return lds_ring_tp[slot];
+}
+
 // computeQueueDelay's outcome for interval [f, s] if the search stops there
 // (queue_model_history_tree.cpp:74-106): op 1 second<-t, 2 first<-t+d+p,
 // 3 remove, 4 split; returns the delay d.
@@ -581,9 +593,14 @@ __device__ __forceinline__ uint64_t tree_case(uint64_t f, uint64_t s, uint64_t t
 // two overridden fields.  head/cnt are the post-prune values and are updated;
 // edited slots are written back.  The ring side that moves is the shorter one
 // (a prefix move shifts `head`): only the logical order is observable.
+// `slot` >= 0: the view is also staged in LDS slot `slot` (ring_dma, logical
+// order), and the range move reads each lane's new intervals from there, at
+// its logical index +-1 (two ds_read_b128, no cross-lane moves); -1: the view
+// came from HBM (ring_load) and the move is a DPP rotate of the registers.
+template <bool LH>
 __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingView& v, uint32_t& head,
                                             uint32_t& cnt, uint64_t t, uint64_t p, uint64_t minp, uint64_t& err,
-                                            uint64_t& f0n, uint64_t& f1n) {
+                                            uint64_t& f0n, uint64_t& f1n, int slot) {
     const int ln = lane_id();
     PROF_T(p_s);
     const uint64_t tp = t + p;
@@ -642,20 +659,33 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
     uint64_t lf = v.lf, ls = v.ls, hf = v.hf, hs = v.hs;
     bool wl = false, wh = false;
     if (rlen) {
-        uint64_t nlf, nls, nhf, nhs;
-        if (next) {
-            ring_shift<true>(v.lf, v.hf, nlf, nhf);
-            ring_shift<true>(v.ls, v.hs, nls, nhs);
-        } else {
-            ring_shift<false>(v.lf, v.hf, nlf, nhf);
-            ring_shift<false>(v.ls, v.hs, nls, nhs);
-        }
         wl = ((jl - r0) & (PU_QRING - 1)) < rlen;
         wh = ((jh - r0) & (PU_QRING - 1)) < rlen;
-        lf = wl ? nlf : lf;
-        ls = wl ? nls : ls;
-        hf = wh ? nhf : hf;
-        hs = wh ? nhs : hs;
+        if (slot >= 0) {
+            // lanes outside the range read their own (unchanged, or dead and
+            // never written back) slot: no select afterwards
+            const v2u64* L = ring_slot<LH>(slot);
+            const uint32_t dn = next ? 1u : PU_QRING - 1;
+            const v2u64 a = L[wl ? (jl + dn) & (PU_QRING - 1) : jl];
+            const v2u64 b = L[wh ? (jh + dn) & (PU_QRING - 1) : jh];
+            lf = a.x;
+            ls = a.y;
+            hf = b.x;
+            hs = b.y;
+        } else {
+            uint64_t nlf, nls, nhf, nhs;
+            if (next) {
+                ring_shift<true>(v.lf, v.hf, nlf, nhf);
+                ring_shift<true>(v.ls, v.hs, nls, nhs);
+            } else {
+                ring_shift<false>(v.lf, v.hf, nlf, nhf);
+                ring_shift<false>(v.ls, v.hs, nls, nhs);
+            }
+            lf = wl ? nlf : lf;
+            ls = wl ? nls : ls;
+            hf = wh ? nhf : hf;
+            hs = wh ? nhs : hs;
+        }
     }
     lf = jl == fi ? fv : lf;
     hf = jh == fi ? fv : hf;
@@ -817,7 +847,7 @@ __device__ __forceinline__ uint64_t q_step(const NetCtx& c, int q, QState& st, u
         RingView v;
         ring_load(c, q, st.head, st.count, v);
         uint64_t f1;
-        d = tree_op(c, q, v, st.head, st.count, t, p, minp, err, st.f0, f1);
+        d = tree_op<LH>(c, q, v, st.head, st.count, t, p, minp, err, st.f0, f1, -1);
         if (st.count >= PU_QMAX) {   // the next call's prune (history_tree.cpp:49-55), done now
             st.head = (st.head + 1) & (PU_QRING - 1);
             st.count--;
@@ -935,17 +965,6 @@ __device__ __forceinline__ int net_route_link(const NetCtx& c, int h, int sx, in
     return inx ? (sz * w + sy) * w1 + ax : iny ? blk + (sz * w + rx) * w1 + ay : 2 * blk + (ry * w + rx) * w1 + az;
 }
 
-// LDS staging ring for predicted tree hops: ring_pf<LH>() full link rings per wave
-// (one wave per workgroup), filled by global_load_lds_dwordx4 and consumed in
-// hop order behind a counted vmcnt (loads, stores and LDS-DMA retire in issue
-// order, MI355X_MICROARCH.md §waitcnt; hipcc would drain everything instead).
-static __shared__ v2u64 lds_ring[PU_RING_PF][PU_QRING];        // latency kernel (LH)
-static __shared__ v2u64 lds_ring_tp[PU_RING_PF_TP][PU_QRING];  // throughput kernels
-template <bool LH>
-__device__ __forceinline__ v2u64* ring_slot(int slot) {
-    if constexpr (LH) return lds_ring[slot];
-    else return lds_ring_tp[slot];
-}
 
 // Stage ring q (live slots [head, head+cnt)) into LDS slot `slot` in logical
 // order; dead positions read the head slot instead (one shared line) and are
@@ -1186,6 +1205,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                 uint64_t f0n, f1n, d;
                 RingView v;
                 const bool staged = mc && jt == (int)__builtin_ctzll(mc);
+                int tslot = -1;
                 if (staged) {
                     // predicted: its ring is (being) staged in LDS slot cslot
                     mc &= mc - 1;
@@ -1197,6 +1217,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                     else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
                     PROF_ADD(PF_NWAIT, p_wait);
                     ring_from_lds<LH>(cslot, v);
+                    tslot = cslot;
                     cslot = cslot == RPF - 1 ? 0 : cslot + 1;
                     consumed++;
                 } else {                            // not predicted (arrival pushed past the front)
@@ -1207,7 +1228,7 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the ring's LDS read, in this region
 #endif
                 PROF_ADD(PF_T_LDS, p_pick);         // hop pick, DMA wait (NWAIT), ring from LDS
-                d = tree_op(c, q, v, head, cnt, tj, (uint64_t)plen, c.link_delay, err, f0n, f1n);
+                d = tree_op<LH>(c, q, v, head, cnt, tj, (uint64_t)plen, c.link_delay, err, f0n, f1n, tslot);
                 PROF_T(p_upd);
                 if (cnt >= PU_QMAX) {               // the next call's prune (history_tree.cpp:49-55), done now
                     head = (head + 1) & (PU_QRING - 1);
