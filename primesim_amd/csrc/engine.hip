@@ -1090,14 +1090,16 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         // (32 B: visit counts, ring cursor, newest finish, the first interval start)
         const int h = b0 + ln;
         const int nh = hops - b0 < 64 ? hops - b0 : 64;
-        int rq = 0;
-        v4u32 ha = v4u32{0, 0, 0, 0}, hb = ha, hc = ha;
+        // Every lane loads: a lane past the route takes the route's last hop,
+        // the same address as that hop's own lane (no extra line, no
+        // exec-masked branch, no zeroed registers); such lanes are masked
+        // wherever a hop's results are used (ln < nh), and their copy of a
+        // real header raises no error that hop does not raise itself.
+        const int rq = net_route_link(c, h < hops ? h : hops - 1, sx, sy, sz, rx, ry, rz, hx, hy);
+        v4u32 ha, hb, hc;
+        hdr_load<LH, WIDE>(c, rq, ha, hb, hc);
         uint64_t vcache = PU_MG1_CACHE_NONE;
-        if (h < hops) {
-            rq = net_route_link(c, h, sx, sy, sz, rx, ry, rz, hx, hy);
-            hdr_load<LH, WIDE>(c, rq, ha, hb, hc);
-            if constexpr (LH) vcache = lds_qcache[rq];
-        }
+        if constexpr (LH) vcache = lds_qcache[rq];
         // Everything about hop h that does not depend on its arrival time is
         // computed by lane h here, once per window: the front interval (the
         // prune of a full history was applied when it filled), the M/G/1 wait
@@ -1303,12 +1305,16 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         hi = wlane<SN_TOTAL>(hi, (uint32_t)(tot >> 32));
         lo = wlane<SN_PLEN>(lo, (uint32_t)plen);
         lo = wlane<SN_FLITS>(lo, (uint32_t)fl);
-        hi = wlane<SN_FLITS>(hi, (uint32_t)(fl >> 32));
+        // mg1 <= hops < 2^9 (at most 65,536 nodes): no high word; flits =
+        // hops x plen has none either while the packed header's two packet
+        // lengths stay below 2^23 (a constant test in a compiled configuration)
+        if (WIDE || (c.p0 | c.p1) >= (1u << 23)) hi = wlane<SN_FLITS>(hi, (uint32_t)(fl >> 32));
         lo = wlane<SN_MG1>(lo, (uint32_t)mg1);
-        hi = wlane<SN_MG1>(hi, (uint32_t)(mg1 >> 32));
         lds_add_u64_lanes(lds_u32addr(&lds_stat[0]) + 8u * (uint32_t)ln, ((uint64_t)hi << 32) | lo, SN_NET_LANES);
     }
-    if (err) err_or(err);
+    // err is per lane (a hop's header state): every bit here is
+    // PU_ERRF_QUEUE, reported if any lane raised it (err_or stores lane 0's)
+    if (ballot(err != 0)) err_or(PU_ERRF_QUEUE);
     PROF_ADD(PF_NPOST, p_post);
     return t - timer;
 }
