@@ -700,9 +700,15 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
     if (wh) R[(head0 + jh) & (PU_QRING - 1)] = v2u64{hf, hs};
     // the header's copies of the first two interval starts: the new cursor is
     // the old logical index (head - head0) & 127 (0, 1 or 127)
-    const uint32_t s0 = (head - head0) & (PU_QRING - 1), s1 = (s0 + 1) & (PU_QRING - 1);
-    f0n = rl64(s0 < 64 ? lf : hf, (int)(s0 & 63));
-    f1n = rl64(s1 < 64 ? lf : hf, (int)(s1 & 63));
+    // (0, 1 or 127: a uniform branch, no selects between the halves)
+    const uint32_t s0 = (head - head0) & (PU_QRING - 1);
+    if (s0 == PU_QRING - 1) {
+        f0n = rl64(hf, 63);
+        f1n = rl64(lf, 0);
+    } else {
+        f0n = rl64(lf, (int)s0);
+        f1n = rl64(lf, (int)s0 + 1);
+    }
     PROF_ADD(PF_T_STORE, p_w);
     return d;
 }
@@ -967,15 +973,17 @@ __device__ __forceinline__ int net_route_link(const NetCtx& c, int h, int sx, in
 
 
 // Stage ring q (live slots [head, head+cnt)) into LDS slot `slot` in logical
-// order; dead positions read the head slot instead (one shared line) and are
-// never used.
+// order; dead positions read the last live slot instead (a line the live
+// part reads anyway) and are never used.
 template <bool LH>
 __device__ __forceinline__ void ring_dma(const NetCtx& c, int q, uint32_t head, uint32_t cnt, int slot) {
     const int ln = lane_id();
     const AS1 v2u64* R = q_ring(c, q);
     // logical order (RingView): LDS position l <- interval l from the cursor
-    const AS1 v2u64* ga = R + ((uint32_t)ln < cnt ? (head + (uint32_t)ln) & (PU_QRING - 1) : head);
-    const AS1 v2u64* gb = R + ((uint32_t)ln + 64 < cnt ? (head + 64 + (uint32_t)ln) & (PU_QRING - 1) : head);
+    // (dead positions re-read the last live slot: min instead of a compare and select)
+    const uint32_t last = cnt - 1;
+    const AS1 v2u64* ga = R + ((head + __builtin_elementwise_min((uint32_t)ln, last)) & (PU_QRING - 1));
+    const AS1 v2u64* gb = R + ((head + __builtin_elementwise_min((uint32_t)ln + 64, last)) & (PU_QRING - 1));
     const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) v2u64*)ring_slot<LH>(slot);
     const uint32_t lo = __builtin_amdgcn_readfirstlane(la), hi = lo + 64 * sizeof(v2u64);
     unsigned keep;
@@ -2638,7 +2646,9 @@ __device__ __forceinline__ bool replica_steps(Engine<NL, LH>& e, const pu_req* _
                                               uint64_t* __restrict__ pos_out) {
     uint64_t i = b;
     for (; i < end; i++) {
-        if (SLICED && __builtin_amdgcn_s_memrealtime() >= uni64(lds_ctl.deadline)) break;
+        // the slice's clock, every fourth request (a slice still ends between
+        // requests, at most three requests later)
+        if (SLICED && (i & 3) == 0 && __builtin_amdgcn_s_memrealtime() >= uni64(lds_ctl.deadline)) break;
         if (uni32((uint32_t)lds_ctl.halted)) break;   // the rest is zero-filled below
         PROF_T(p_loop);
         const uint32_t fl = uni32(lds_ctl.flags);

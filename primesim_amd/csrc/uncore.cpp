@@ -932,6 +932,7 @@ uint64_t pu_replica_pool_bytes(const pu_handle* h) {
     return h ? (uint64_t)h->geo.dir.pool_entries * ((uint64_t)h->geo.dir.nwords * 8 + 4) : 0;
 }
 
+extern "C++" {   // inside the C-ABI block: these helpers keep C++ linkage
 namespace pu {
 // The device's target name ("gfx950" from "gfx950:sramecc+:xnack-").
 std::string device_target(int device) {
@@ -954,6 +955,7 @@ int lds_limited_per_cu(int lds_bytes, int lds_per_cu, int granule) {
     return lds_per_cu / unit;
 }
 }  // namespace pu
+}  // extern "C++"
 
 int pu_resident_replicas(const pu_handle* h) {
     if (!h) return pu::set_error(PU_EINVAL, "null handle");
