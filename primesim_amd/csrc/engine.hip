@@ -94,6 +94,32 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
 // lane l of v becomes x (x wave-uniform)
 __device__ __forceinline__ uint32_t wl32(uint32_t v, uint32_t x, int l) { return lane_id() == l ? x : v; }
 __device__ __forceinline__ uint64_t wl64(uint64_t v, uint64_t x, int l) { return lane_id() == l ? x : v; }
+// A tree hop's results into lane l of the window's per-hop registers: one
+// v_writelane_b32 per dword (a lane compare and a select per dword in
+// wl32/wl64; clang has no writelane builtin here).  The lane select goes
+// through M0, saved and restored as ring_dma does (an SGPR lane select and
+// SGPR data would take the constant bus twice); s_nop 3 covers a
+// VALU-written lane select (4 wait states on CDNA).
+__device__ __forceinline__ void wl_hop(uint32_t& a, uint32_t xa, uint32_t& b, uint32_t xb, uint64_t& c, uint64_t xc,
+                                       uint64_t& d, uint64_t xd, int l) {
+    uint32_t c0 = (uint32_t)c, c1 = (uint32_t)(c >> 32), d0 = (uint32_t)d, d1 = (uint32_t)(d >> 32);
+    uint32_t keep;
+    asm("s_mov_b32 %6, m0\n\t"
+        "s_mov_b32 m0, %13\n\t"
+        "s_nop 3\n\t"
+        "v_writelane_b32 %0, %7, m0\n\t"
+        "v_writelane_b32 %1, %8, m0\n\t"
+        "v_writelane_b32 %2, %9, m0\n\t"
+        "v_writelane_b32 %3, %10, m0\n\t"
+        "v_writelane_b32 %4, %11, m0\n\t"
+        "v_writelane_b32 %5, %12, m0\n\t"
+        "s_mov_b32 m0, %6"
+        : "+v"(a), "+v"(b), "+v"(c0), "+v"(c1), "+v"(d0), "+v"(d1), "=&s"(keep)
+        : "s"(xa), "s"(xb), "s"((uint32_t)xc), "s"((uint32_t)(xc >> 32)), "s"((uint32_t)xd),
+          "s"((uint32_t)(xd >> 32)), "s"(l));
+    c = ((uint64_t)c1 << 32) | c0;
+    d = ((uint64_t)d1 << 32) | d0;
+}
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ uint32_t uni32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
@@ -619,9 +645,14 @@ __device__ __forceinline__ uint64_t tree_op(const NetCtx& c, int q, const RingVi
     PROF_ADD(PF_T_SEARCH, p_s);
     PROF_T(p_d);
     // the outcome for the found interval only, on the scalar unit
-    const bool hi_half = k >= 64;
-    const uint64_t sf = rl64(hi_half ? v.hf : v.lf, (int)(k & 63));
-    const uint64_t ss = rl64(hi_half ? v.hs : v.ls, (int)(k & 63));
+    uint64_t sf, ss;
+    if (k >= 64) {              // uniform: no selects between the halves
+        sf = rl64(v.hf, (int)(k - 64));
+        ss = rl64(v.hs, (int)(k - 64));
+    } else {
+        sf = rl64(v.lf, (int)k);
+        ss = rl64(v.ls, (int)k);
+    }
     uint32_t op;
     const uint64_t d = tree_case(sf, ss, t, p, minp, op);
     // the edit as: slots whose logical index is in [r0, r0+rlen) take their
@@ -1255,12 +1286,9 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
                     PROF_ADD(PF_T_REFILL, p_r);
                 }
                 sh += d - rl64(vd, jt);
-                vhead = wl32(vhead, head, jt);
-                vcnt = wl32(vcnt, cnt, jt);
-                vf0 = wl64(vf0, f0n, jt);
                 // (hop jt's assumed wait vd is not read again: later M/G/1 finish
                 // times and shifts use the lanes after it)
-                vfin = wl64(vfin, tj + d + (uint64_t)plen, jt);
+                wl_hop(vhead, head, vcnt, cnt, vf0, f0n, vfin, tj + d + (uint64_t)plen, jt);
                 t = tj + d + c.link_delay;
                 js = jt + 1;
                 PROF_ADD(PF_T_UPD, p_upd);          // prune, refill (T_REFILL), hop results into the window
