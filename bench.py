@@ -97,9 +97,9 @@ WORKLOADS = {
                    "full-map; producer/consumer pairs (p, p+2048) sharing 1,024-line buffers, 50% writes"},
 }
 WORKLOAD = "C4"         # set by main() before the ensemble forks (its workers read it)
-LIMITER = ("dependent-load latency and instruction issue (profiles/r6i_sq.json: 25.6% of wave cycles issuing, "
-           "38.6% waiting on memory, 35.8% in issue stalls at 7 waves/SIMD, 1,360 VALU + 1,337 SALU per access; "
-           "fabric traffic about 41% of 8 TB/s), not HBM bandwidth")
+LIMITER = ("dependent-load latency and instruction issue (profiles/r6r_sq.json: 25.4% of wave cycles issuing, "
+           "39.3% waiting on memory, 35.4% in issue stalls at 7 waves/SIMD, 1,235 VALU + 1,330 SALU per access; "
+           "fabric traffic about 43% of 8 TB/s), not HBM bandwidth")
 REQ_BYTES = 32          # sizeof(pu_req)
 VARIANTS = {0: "ahead-of-time kernels (runtime geometry) for every launch",
             1: "ahead-of-time kernels for the replicas (throughput launches); the configuration compiled into "
