@@ -1153,18 +1153,25 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         // its tag is this header's n, else computed here (latency mode), or
         // computed here (throughput mode)
         uint64_t vd = 0;
-        bool need = ln < nh;
+        [[maybe_unused]] bool need = ln < nh;
         if constexpr (LH) {
             const uint64_t wmask = (1ull << PU_MG1_WAIT_BITS) - 1;
             const bool hit = need && (vcache & wmask) != wmask && hs.n < 4294967296.0 &&
                              ((uint32_t)(vcache >> PU_MG1_WAIT_BITS) ^ (uint32_t)vcache) == (uint32_t)hs.n;
             if (hit) vd = vcache & wmask;
             need = need && !hit;
-        }
-        if (ballot(need)) {
+            if (ballot(need)) {
+                PROF_T(p_mg1);
+                const uint64_t w = mg1_wait(hs);
+                if (need) vd = w;
+                PROF_ADD(PF_MG1RUN, p_mg1);
+            }
+        } else {
+            // every lane: a lane past the route holds a copy of the route's last
+            // hop, and its wait only reaches lanes above the route in the
+            // inclusive scan below (no mask, no select)
             PROF_T(p_mg1);
-            const uint64_t w = mg1_wait(hs);
-            if (need) vd = w;
+            vd = mg1_wait(hs);
             PROF_ADD(PF_MG1RUN, p_mg1);
         }
         PROF_CNT(PF_MG1LANES, (uint64_t)nh);
@@ -1175,12 +1182,10 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         // (queue delays are >= 0).  A hop whose front free interval starts by
         // LB_j + p cannot take the M/G/1 branch, so its full ring is certainly
         // needed: stage those rings now, ring_pf<LH>() ahead, in hop order.
-        bool pred = false;
-        if (ln < nh) {
-            const uint64_t lb = t + (uint64_t)(ln + 1) * c.router + (uint64_t)ln * c.link_delay;
-            pred = vfront <= lb + (uint64_t)plen;
-        }
-        const uint64_t M = ballot(pred);
+        // (every lane computes; the mask drops the lanes past the route)
+        const uint64_t nhm = nh >= 64 ? ~0ull : ((1ull << nh) - 1);
+        const uint64_t lb = t + (uint64_t)(ln + 1) * c.router + (uint64_t)ln * c.link_delay;
+        const uint64_t M = ballot(vfront <= lb + (uint64_t)plen) & nhm;
         uint64_t mi = M, mc = M;        // issue / consume cursors over the predicted hops
         int issued = 0, consumed = 0;
         constexpr int RPF = ring_pf<LH>();
@@ -1208,7 +1213,9 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
         uint64_t S = 0, A0 = 0, sh = 0;
         const uint64_t t0 = t;
         {
-            const uint64_t e = ln < nh ? vd + c.link_delay + c.router : 0;
+            // lanes past the route add their copies' terms above it: an
+            // inclusive scan never carries them down
+            const uint64_t e = vd + c.link_delay + c.router;
             S = ballot(e >= (1ull << 26)) == 0 ? (uint64_t)scan_incl_u32((uint32_t)e) : scan_incl_u64(e);
             A0 = t + c.router + (S - e);
         }
@@ -1222,7 +1229,6 @@ __device__ __forceinline__ uint64_t net_transmit(const Geo* __restrict__ g, char
             // operation on wave masks, tree_op's predicates combined on the
             // scalar unit, ran 9% slower closed loop: more scalar
             // instructions than it saved)
-            const uint64_t nhm = nh >= 64 ? ~0ull : ((1ull << nh) - 1);
             int islot = issued % RPF, cslot = 0;
             while (js < nh) {
                 const uint64_t live = nhm & (~0ull << js);
