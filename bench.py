@@ -97,8 +97,8 @@ WORKLOADS = {
                    "full-map; producer/consumer pairs (p, p+2048) sharing 1,024-line buffers, 50% writes"},
 }
 WORKLOAD = "C4"         # set by main() before the ensemble forks (its workers read it)
-LIMITER = ("dependent-load latency and instruction issue (profiles/r6r_sq.json: 25.4% of wave cycles issuing, "
-           "39.3% waiting on memory, 35.4% in issue stalls at 7 waves/SIMD, 1,235 VALU + 1,330 SALU per access; "
+LIMITER = ("dependent-load latency and instruction issue (profiles/r6y_sq.json: 25.3% of wave cycles issuing, "
+           "39.6% waiting on memory, 35.1% in issue stalls at 7 waves/SIMD, 1,210 VALU + 1,339 SALU per access; "
            "fabric traffic about 43% of 8 TB/s), not HBM bandwidth")
 REQ_BYTES = 32          # sizeof(pu_req)
 VARIANTS = {0: "ahead-of-time kernels (runtime geometry) for every launch",
